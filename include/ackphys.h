@@ -1,0 +1,89 @@
+/* ackphys.h -- C-ABI of libackphys.so, the MI355X batched physics step for the
+ * ackermann_robot_v2 environment.
+ *
+ * This is the drop-in boundary that replaces, for N environments at once, the reference's
+ * per-env call chain (one Python env per process, src/rl/train.py:73-76):
+ *
+ *   AckermannRobotEnv.step(action)            src/rl/envs/ackermann_env.py:187-229
+ *     BicycleController.apply_cmd_vel         src/core/controller.py:136-140 (98-134)
+ *     mujoco.mj_step(model, data)             src/rl/envs/ackermann_env.py:200
+ *     _get_observation / _calculate_reward    src/rl/envs/ackermann_env.py:231-312
+ *   AckermannRobotEnv.reset()                 src/rl/envs/ackermann_env.py:143-185
+ *     SimpleMapSpawner.load_random_environment src/rl/envs/simple_map_spawner.py:22-54
+ *
+ * Conventions
+ *  - All array arguments are DEVICE pointers owned by the caller (torch tensors in the
+ *    Python host layer); the library never allocates per call and never synchronises.
+ *  - Work is enqueued on `stream` (a hipStream_t passed as void*; NULL = default stream).
+ *  - Every entry point returns 0 on success or a negative ACKPHYS_E* code; the message is
+ *    available from ackphys_last_error() (thread-local).
+ *
+ * Layouts (N = n_env given to ackphys_create; all float32 unless noted)
+ *  state  [44][N]  word k of env e at state[k*N + e]:
+ *           0-12 qpos (free joint xyz + quat wxyz, 6 hinges), 13-24 qvel, 25-36 qacc_warmstart,
+ *           37-38 goal xy, 39-41 odometry reference xyz, 42 step_count (uint32 bits),
+ *           43 episode counter (uint32 bits)
+ *  action [N][2]   normalised (linear_x, angular_z) in [-1,1] (clipped like the reference)
+ *  obs    [79][N]  72 lidar, x, y, yaw, dx, dy, dist, angle (ackermann_env.py:231-265)
+ *  reward [N], term [N] (uint8), trunc [N] (uint8)
+ *  terminal_obs [79][N] (nullable): observation before auto-reset, written for done envs
+ *  info   [4][N]  (nullable): min_lidar, collision, goal_distance, bad_state
+ */
+#ifndef ACKPHYS_H
+#define ACKPHYS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ackphys_ctx ackphys_t;
+
+#define ACKPHYS_NSTATE 44
+#define ACKPHYS_NOBS 79
+
+/* step flags */
+#define ACKPHYS_CONTACTS 1u  /* 0 = MJCF <flag contact="disable"/> (BASELINE config 2) */
+#define ACKPHYS_AUTORESET 2u /* SB3 VecEnv semantics: reset done envs inside the step */
+
+/* error codes */
+#define ACKPHYS_OK 0
+#define ACKPHYS_EINVAL -1
+#define ACKPHYS_EMODEL -2
+#define ACKPHYS_EHIP -3
+
+/* Create a context for n_env environments on HIP device `device`.
+ * model_blob: the compiled model (include/ackphys_model.h), i.e. what the reference
+ * builds with mujoco.MjModel.from_xml_path (simple_map_spawner.py:37). The library's kernels
+ * are specialised on one model; a blob that does not match it is rejected (ACKPHYS_EMODEL). */
+int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device, ackphys_t** out);
+int ackphys_destroy(ackphys_t* ctx);
+
+/* Global index of this context's env 0 (multi-GPU sharding: rank r passes r*n_env); it keys
+ * the Philox streams for goals so a sharded run is identical to an unsharded one. */
+int ackphys_set_env_offset(ackphys_t* ctx, int64_t env_offset);
+
+/* One environment step for all N envs (replaces AckermannRobotEnv.step). */
+int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, float* reward, uint8_t* term,
+                 uint8_t* trunc, float* terminal_obs, float* info, uint32_t flags, uint64_t seed, void* stream);
+
+/* Reset the envs whose mask byte is non-zero (mask NULL = all) (replaces
+ * AckermannRobotEnv.reset): spawner pose, zero velocities, Philox(seed, env, episode) goal,
+ * observation at the reset state. */
+int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* state, float* obs, void* stream);
+
+/* Fill actions[K][N][2] with i.i.d. U[-1,1) from Philox4x32-10 keyed by seed, counter
+ * (env_offset + env, step0 + k, 1, 0): the benchmark's synthetic "random ctrl" input. */
+int ackphys_random_actions(ackphys_t* ctx, float* actions, int k_steps, uint64_t seed, uint32_t step0, void* stream);
+
+/* FNV-1a 64 of the model blob the kernels were specialised on. */
+uint64_t ackphys_model_fnv(void);
+const char* ackphys_last_error(void);
+const char* ackphys_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACKPHYS_H */

@@ -1,0 +1,85 @@
+"""Loader for libackphys.so (the HIP C-ABI, include/ackphys.h) and its in-tree build.
+
+There is no CPU fallback: if the library is missing or cannot be loaded the product raises.
+(The CPU oracle under oracle/ is test infrastructure and is never imported here.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB_PATH = os.path.join(CSRC, "build", "libackphys.so")
+REPO = os.path.dirname(PKG)
+SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_model_gen.h"),
+           os.path.join(REPO, "include", "ackphys.h"), os.path.join(REPO, "include", "ackphys_model.h")]
+BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-fast-math",
+               "-Wno-unused-result"]
+
+
+class ExtensionMissing(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    """Compile csrc/ackphys_step.hip for gfx950 into csrc/build/libackphys.so (in-tree)."""
+    if not force and os.path.exists(LIB_PATH):
+        t = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(s) <= t for s in SOURCES):
+            return LIB_PATH
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "ackphys_step.hip")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    if verbose:
+        print(f"built {LIB_PATH}")
+    return LIB_PATH
+
+
+EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
+           "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
+
+_lib = None
+
+
+def lib():
+    """The loaded C-ABI; raises ExtensionMissing if the HIP build is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ExtensionMissing(f"{LIB_PATH} not found: build it with `python -c \"import __graft_entry__ as g; "
+                               f"g.build()\"` (hipcc --offload-arch=gfx950)")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:
+        raise ExtensionMissing(f"cannot load {LIB_PATH}: {e}") from e
+    P, i32, i64, u32, u64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_size_t
+    L.ackphys_create.argtypes = [C.c_char_p, sz, i32, i32, C.POINTER(P)]
+    L.ackphys_destroy.argtypes = [P]
+    L.ackphys_set_env_offset.argtypes = [P, i64]
+    L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, u32, u64, P]
+    L.ackphys_reset.argtypes = [P, P, u64, P, P, P]
+    L.ackphys_random_actions.argtypes = [P, P, i32, u64, u32, P]
+    L.ackphys_model_fnv.restype = u64
+    L.ackphys_last_error.restype = C.c_char_p
+    L.ackphys_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def load_blob() -> bytes:
+    with open(BLOB_PATH, "rb") as f:
+        return f.read()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {lib().ackphys_last_error().decode()}")

@@ -1,0 +1,1388 @@
+// ackphys_step.hip -- MI355X (gfx950) batched physics step for ackermann_robot_v2.
+//
+// One wavefront lane per environment. Each lane runs the whole reference step for its env
+// (src/rl/envs/ackermann_env.py:187-229):
+//   controller (f64, src/core/controller.py:98-140) -> checkPos/Vel -> kinematics -> lidar /
+//   odometry / obs / reward (pre-integration, ackermann_env.py:231-312) -> composite inertia +
+//   Newton-Euler bias in CHASSIS-FRAME coordinates -> passive + actuators -> plane-cylinder and
+//   plane-convex contacts -> equality / friction-loss / limit / pyramidal-contact rows ->
+//   primal Newton solve (exact piecewise-quadratic line search) -> implicit-damping Euler ->
+//   auto-reset with Philox goals (ackermann_env.py:143-185).
+//
+// Layout: state/obs are SoA [word][N] so every global access is lane-contiguous (coalesced);
+// actions are AoS [N][2] (8 B per lane, also contiguous). Per-contact-slot scratch lives in
+// LDS as [slot][field][lane] (bank-conflict-free, wave-uniform slot loops).
+//
+// Coordinates: u = (v_b, w_b, qdot_hinges) with v_b = R^T v_world. In u every CoM is fixed in
+// the chassis frame and every wheel/steer inertia is isotropic (checked by codegen.py), so the
+// 12x12 mass matrix is constant except the two front spin-axis couplings. The constraint
+// problem is the same convex program as MuJoCo's (cost is invariant under u = T q, T orthogonal).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ackphys_model_gen.h"
+
+namespace ak {
+using namespace apg;
+
+constexpr int NV = 12;
+constexpr int NSTATE = 44;
+constexpr int NOBS = 79;
+constexpr int ST_QPOS = 0, ST_QVEL = 13, ST_WARM = 25, ST_GOAL = 37, ST_REF = 39, ST_STEP = 42, ST_EPIS = 43;
+constexpr uint32_t F_CONTACTS = 1u, F_AUTORESET = 2u;
+constexpr int NSLOT = 24;        // 4 wheels x 4 + 2 meshes x 4 contact slots
+constexpr int NF = 13;           // Pb[3], D, jar[4], jp[4], active
+constexpr int NSCAL = 11;        // eq(1) + frictionloss(6) + limits(4)
+constexpr int MAXIT = 16;        // Newton iterations cap (MuJoCo: 100; converges in 1-4 here)
+constexpr int LSIT = 12;         // line-search iterations cap
+constexpr float MINVAL = 1e-15f;
+
+// env constants (ackermann_env.py:51-60; controller.py:85-86)
+constexpr int MAX_STEPS = 1000;
+constexpr float GOAL_THRESH = 0.5f, COLL_THRESH = 0.15f;
+
+struct Args {
+  const float* action;
+  float* state;
+  float* obs;
+  float* reward;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* tobs;
+  float* info;
+  int n;
+  uint32_t flags;
+  uint64_t seed;
+  int64_t env_offset;
+};
+
+// ------------------------------------------------------------------ small helpers
+__device__ __forceinline__ float sq(float x) { return x * x; }
+__device__ __forceinline__ void cross(float r[3], const float a[3], const float b[3]) {
+  r[0] = a[1] * b[2] - a[2] * b[1];
+  r[1] = a[2] * b[0] - a[0] * b[2];
+  r[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ __forceinline__ float dot(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }  // NaN or huge
+
+// Philox4x32-10 (Random123); identical to oracle/ackphys_oracle.c
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// ------------------------------------------------------------------ controller (f64)
+// BicycleController.cmd_vel_to_controls + apply_cmd_vel, controller.py:98-140, evaluated in
+// float64 exactly like the reference (its thresholds 1e-6 / 1e-5 sit on f64 values).
+__device__ void controller(float a0f, float a1f, float ctrl[3], bool& bad) {
+  double a0 = a0f, a1 = a1f;
+  a0 = a0 < -1.0 ? -1.0 : (a0 > 1.0 ? 1.0 : a0);
+  a1 = a1 < -1.0 ? -1.0 : (a1 > 1.0 ? 1.0 : a1);
+  const double L = 0.20, T = 0.174, rw = 0.0325, eps = 1e-5;
+  double v = a0 * 1.0, om = a1 * 1.0, delta;
+  if (fabs(om) < 1e-6) delta = 0.0;
+  else {
+    double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
+    delta = atan((L * om) / den);
+  }
+  const double lim = 35.0 * (3.141592653589793 / 180.0);
+  delta = delta < -lim ? -lim : (delta > lim ? lim : delta);
+  double vl, vr;
+  if (fabs(delta) < 1e-6) vl = vr = v;
+  else {
+    double t = tan(delta);
+    double R = fabs(t) > eps ? L / t : __builtin_inf();
+    double wt = fabs(R) > eps ? v / R : 0.0;
+    vl = wt * (R - T / 2.0);   // 0*inf = NaN, as in the reference
+    vr = wt * (R + T / 2.0);
+  }
+  double wl = vl / rw, wr = vr / rw;
+  double c0 = delta < -0.61 ? -0.61 : (delta > 0.61 ? 0.61 : delta);
+  double c1 = (wl != wl) ? wl : (wl < -50 ? -50 : (wl > 50 ? 50 : wl));
+  double c2 = (wr != wr) ? wr : (wr < -50 ? -50 : (wr > 50 ? 50 : wr));
+  bad = !(fabs(c0) <= 1e10) || !(fabs(c1) <= 1e10) || !(fabs(c2) <= 1e10);
+  if (bad) c0 = c1 = c2 = 0.0;  // MuJoCo zeroes ctrl on bad values
+  ctrl[0] = (float)c0; ctrl[1] = (float)c1; ctrl[2] = (float)c2;
+}
+
+// ------------------------------------------------------------------ kinematics
+__device__ __forceinline__ void quat_R(const float q[4], float R[9]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void normq(float q[4]) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else { float inv = 1.0f / n; q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv; }
+}
+// rotate v about unit axis s by angle (Rodrigues): the steer rotation of front-wheel frames
+__device__ __forceinline__ void rot_axis(float r[3], const float s[3], const float v[3], float c, float sn) {
+  float sxv[3];
+  cross(sxv, s, v);
+  float sv = dot(s, v) * (1 - c);
+#pragma unroll
+  for (int k = 0; k < 3; k++) r[k] = v[k] * c + sxv[k] * sn + s[k] * sv;
+}
+
+// ------------------------------------------------------------------ observation + reward
+// _get_observation / _calculate_reward (ackermann_env.py:231-312) on the PRE-integration pose
+// (mj_step's sensors and xpos/xquat come from its mj_forward). Lidar: rays are horizontal in
+// the chassis frame at RAY_Z and every robot geom lies below that plane (codegen.py proves it),
+// so only the floor can be hit: mj_ray's plane test with the 40x40 rectangle, cutoff clamp.
+struct ObsOut { float minl, dist, reward; bool term, coll; };
+
+__device__ ObsOut observe_head(const float p[3], const float q[4], const float R[9], float gx, float gy,
+                               const float ref[3], float out8[7]) {
+  // odometry (odometry.py:62-103, 154-170)
+  float x = p[0] - ref[0], y = p[1] - ref[1];
+  float yaw = atan2f(2 * (q[0] * q[3] + q[1] * q[2]), 1 - 2 * (q[2] * q[2] + q[3] * q[3]));
+  float dx = gx - x, dy = gy - y;
+  float dist = sqrtf(dx * dx + dy * dy);
+  float ang = atan2f(dy, dx) - yaw;
+  ang = atan2f(sinf(ang), cosf(ang));
+  out8[0] = x; out8[1] = y; out8[2] = yaw; out8[3] = dx; out8[4] = dy; out8[5] = dist; out8[6] = ang;
+  ObsOut o;
+  o.dist = dist;
+  o.term = dist < GOAL_THRESH;
+  return o;
+}
+
+__device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
+  // site origin / direction (chassis frame) -> world; mj_ray plane test (ray_plane)
+  const float ox = RAY_ORG[i][0], oy = RAY_ORG[i][1], dxb = RAY_DIR[i][0], dyb = RAY_DIR[i][1];
+  float dz = R[6] * dxb + R[7] * dyb;
+  float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
+  if (dz > -MINVAL) return -1.0f;
+  float t = -oz / dz;
+  if (t < 0) return -1.0f;
+  float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
+  float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
+  if (fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1]) return fminf(t, RAY_CUTOFF);
+  return -1.0f;
+}
+
+// writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
+__device__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
+                          const float ref[3], float* dst, int n) {
+  float head[7];
+  ObsOut o = observe_head(p, q, R, gx, gy, ref, head);
+  // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
+  // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
+  float minl = 3.0e38f, v71 = -1.0f;
+#pragma unroll 2
+  for (int i = 10; i < 72; i++) {
+    float v = ray_floor(p, R, i);
+    dst[(size_t)i * n] = v;
+    minl = fminf(minl, v);
+    v71 = v;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) dst[(size_t)i * n] = v71;
+#pragma unroll
+  for (int k = 0; k < 7; k++) dst[(size_t)(72 + k) * n] = head[k];
+  o.minl = minl;
+  o.coll = minl < COLL_THRESH;
+  float r = 0.0f;
+  r -= o.dist * 0.1f;
+  if (o.term) r += 100.0f;
+  if (o.coll) r -= 50.0f;
+  r -= 0.01f;
+  o.reward = r;
+  return o;
+}
+
+// ------------------------------------------------------------------ impedance / reference
+__device__ __forceinline__ float impedance(float pos) {
+  // getimpedance: solimp (d0, dmax, width, mid, power), margin 0
+  const float d0 = SOLIMP[0], dmax = SOLIMP[1], width = SOLIMP[2], mid = SOLIMP[3], pw = SOLIMP[4];
+  float x = fabsf(pos) / width;
+  if (x >= 1.0f) return dmax;
+  float y;
+  if (pw == 1.0f) y = x;
+  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1.0f);
+  else y = 1.0f - powf(1.0f - x, pw) / powf(1.0f - mid, pw - 1.0f);
+  float imp = d0 + y * (dmax - d0);
+  return fminf(fmaxf(imp, 0.0001f), 0.9999f);
+}
+// K, B from solref (refsafe: timeconst >= 2*dt)
+__device__ __forceinline__ void ref_kb(float& K, float& B) {
+  const float dmax = SOLIMP[1];
+  const float tc = SOLREF[0] > 2.0f * DT ? SOLREF[0] : 2.0f * DT;
+  const float dr = SOLREF[1];
+  K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+  B = 2.0f / (dmax * tc);
+}
+
+// ------------------------------------------------------------------ 12x12 Cholesky
+__device__ __forceinline__ bool chol12(float A[NV][NV]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    float s = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= A[j][k] * A[j][k];
+    ok = ok && (s > 0.0f);
+    s = sqrtf(fmaxf(s, 1e-30f));
+    A[j][j] = s;
+    float inv = 1.0f / s;
+#pragma unroll
+    for (int i = j + 1; i < NV; i++) {
+      float t = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= A[i][k] * A[j][k];
+      A[i][j] = t * inv;
+    }
+  }
+  return ok;
+}
+__device__ __forceinline__ void chol12_solve(const float L[NV][NV], float x[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    float s = x[i];
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[i][k] * x[k];
+    x[i] = s / L[i][i];
+  }
+#pragma unroll
+  for (int i = NV - 1; i >= 0; i--) {
+    float s = x[i];
+#pragma unroll
+    for (int k = i + 1; k < NV; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+}
+__device__ __forceinline__ void symv12(const float M[NV][NV], const float x[NV], float y[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    float s = 0;
+#pragma unroll
+    for (int j = 0; j < NV; j++) s += (j <= i ? M[i][j] : M[j][i]) * x[j];
+    y[i] = s;
+  }
+}
+
+// ------------------------------------------------------------------ mass matrix (u coords)
+// Lower triangle. Constant except the front spin couplings (axis a(delta) in chassis frame).
+__device__ __forceinline__ void build_M(float M[NV][NV], const float sa[2][3]) {
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < NV; j++) M[i][j] = 0.0f;
+  M[0][0] = M[1][1] = M[2][2] = M_TOT;
+  // M_{w v} = m [c]x  (lower block rows 3..5, cols 0..2)
+  const float cx = C_TOT[0], cy = C_TOT[1], cz = C_TOT[2];
+  M[3][1] = -M_TOT * cz; M[3][2] = M_TOT * cy;
+  M[4][0] = M_TOT * cz; M[4][2] = -M_TOT * cx;
+  M[5][0] = -M_TOT * cy; M[5][1] = M_TOT * cx;
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) M[3 + a][3 + b] = I_O[a][b];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int ds = W_SPIN_DOF[w];
+    if (W_STEER_DOF[w] < 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) M[ds][3 + k] = W_I[w] * W_SPIN_AXIS[w][k];
+      M[ds][ds] = W_I[w] + ARMATURE[ds];
+    } else {
+      const int st = W_STEER_DOF[w], s = w - 2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) M[st][3 + k] = (S_I[s] + W_I[w]) * S_AXIS[s][k];
+      M[st][st] = S_I[s] + W_I[w] + ARMATURE[st];
+#pragma unroll
+      for (int k = 0; k < 3; k++) M[ds][3 + k] = W_I[w] * sa[s][k];
+      M[ds][st] = W_I[w] * dot(S_AXIS[s], sa[s]);
+      M[ds][ds] = W_I[w] + ARMATURE[ds];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ bias forces (RNE, u coords)
+// qfrc_bias = Coriolis/centrifugal/gyroscopic + gravity, Newton-Euler per body in the chassis
+// frame with zero generalised acceleration (MuJoCo mj_rne with flg_acc = 0).
+__device__ void bias(const float u[NV], const float R[9], const float sa[2][3], float b[NV]) {
+  const float w[3] = {u[3], u[4], u[5]};
+  // gravity in the chassis frame
+  const float g[3] = {R[0] * GRAV[0] + R[3] * GRAV[1] + R[6] * GRAV[2], R[1] * GRAV[0] + R[4] * GRAV[1] + R[7] * GRAV[2],
+                      R[2] * GRAV[0] + R[5] * GRAV[1] + R[8] * GRAV[2]};
+#pragma unroll
+  for (int i = 0; i < NV; i++) b[i] = 0.0f;
+  // chassis group
+  {
+    float wxr[3], a[3], f[3], Iw[3], gy[3], rxf[3];
+    cross(wxr, w, C_G);
+    cross(a, w, wxr);
+#pragma unroll
+    for (int k = 0; k < 3; k++) f[k] = M_G * (a[k] - g[k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) Iw[k] = I_G[k][0] * w[0] + I_G[k][1] * w[1] + I_G[k][2] * w[2];
+    cross(gy, w, Iw);
+    cross(rxf, C_G, f);
+#pragma unroll
+    for (int k = 0; k < 3; k++) { b[k] += f[k]; b[3 + k] += rxf[k] + gy[k]; }
+  }
+#pragma unroll
+  for (int wi = 0; wi < 4; wi++) {
+    const float* r = W_ANCHOR[wi];
+    float wxr[3], a[3], f[3], rxf[3];
+    cross(wxr, w, r);
+    cross(a, w, wxr);
+    const float ms = W_M[wi] + (W_STEER_DOF[wi] >= 0 ? S_M[wi - 2 < 0 ? 0 : wi - 2] : 0.0f);
+#pragma unroll
+    for (int k = 0; k < 3; k++) f[k] = ms * (a[k] - g[k]);
+    cross(rxf, r, f);
+    float tau[3];
+    const int ds = W_SPIN_DOF[wi];
+    if (W_STEER_DOF[wi] < 0) {
+      // alpha = w x a qdot ; isotropic: no gyroscopic torque
+      float wxa[3];
+      cross(wxa, w, W_SPIN_AXIS[wi]);
+#pragma unroll
+      for (int k = 0; k < 3; k++) tau[k] = W_I[wi] * wxa[k] * u[ds];
+      b[ds] += dot(W_SPIN_AXIS[wi], tau);
+    } else {
+      const int st = W_STEER_DOF[wi], s = wi - 2;
+      const float* sax = S_AXIS[s];
+      const float* ax = sa[s];
+      float wxs[3], ws[3], wsxa[3];
+      cross(wxs, w, sax);
+#pragma unroll
+      for (int k = 0; k < 3; k++) ws[k] = w[k] + sax[k] * u[st];
+      cross(wsxa, ws, ax);
+      float ts[3], tw[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        ts[k] = S_I[s] * wxs[k] * u[st];
+        tw[k] = W_I[wi] * (wxs[k] * u[st] + wsxa[k] * u[ds]);
+        tau[k] = ts[k] + tw[k];
+      }
+      b[st] += dot(sax, tau);
+      b[ds] += dot(ax, tw);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) { b[k] += f[k]; b[3 + k] += rxf[k] + tau[k]; }
+  }
+}
+
+// ------------------------------------------------------------------ contact slots in LDS
+struct Slots {
+  float* base;  // [NSLOT][NF][64] for this block; lane offset applied
+  __device__ __forceinline__ float& at(int s, int f) const { return base[(s * NF + f) * 64]; }
+};
+
+// chain geometry: contact point P (chassis frame) -> jacobian rows G[dir][8] for the 3 frame
+// directions; columns 0..5 = v_b, w_b; col 6/7 = chain hinge dofs (see dof6/dof7).
+template <int CH>
+struct Chain {
+  static constexpr bool wheel = CH < 4;
+  static constexpr bool front = CH == 2 || CH == 3;
+  static constexpr int dof6 = !wheel ? -1 : (front ? W_STEER_DOF[CH] : W_SPIN_DOF[CH]);
+  static constexpr int dof7 = front ? W_SPIN_DOF[CH] : -1;
+};
+
+template <int CH>
+__device__ __forceinline__ void jac_rows(const float P[3], const float dirs[3][3], const float sa[2][3],
+                                         float G[3][8]) {
+  float c6[3] = {0, 0, 0}, c7[3] = {0, 0, 0};
+  if constexpr (Chain<CH>::wheel) {
+    float rel[3] = {P[0] - W_ANCHOR[CH][0], P[1] - W_ANCHOR[CH][1], P[2] - W_ANCHOR[CH][2]};
+    if constexpr (Chain<CH>::front) {
+      cross(c6, S_AXIS[CH - 2], rel);
+      cross(c7, sa[CH - 2], rel);
+    } else {
+      cross(c6, W_SPIN_AXIS[CH], rel);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const float* db = dirs[d];
+    float pxd[3];
+    cross(pxd, P, db);
+    G[d][0] = db[0]; G[d][1] = db[1]; G[d][2] = db[2];
+    G[d][3] = pxd[0]; G[d][4] = pxd[1]; G[d][5] = pxd[2];
+    G[d][6] = dot(c6, db);
+    G[d][7] = dot(c7, db);
+  }
+}
+
+template <int CH>
+__device__ __forceinline__ float row_dot(const float J[8], const float x[NV]) {
+  float s = J[0] * x[0] + J[1] * x[1] + J[2] * x[2] + J[3] * x[3] + J[4] * x[4] + J[5] * x[5];
+  if constexpr (Chain<CH>::dof6 >= 0) s += J[6] * x[Chain<CH>::dof6];
+  if constexpr (Chain<CH>::dof7 >= 0) s += J[7] * x[Chain<CH>::dof7];
+  return s;
+}
+template <int CH>
+__device__ __forceinline__ void row_axpy(const float J[8], float f, float g[NV]) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) g[k] += f * J[k];
+  if constexpr (Chain<CH>::dof6 >= 0) g[Chain<CH>::dof6] += f * J[6];
+  if constexpr (Chain<CH>::dof7 >= 0) g[Chain<CH>::dof7] += f * J[7];
+}
+template <int CH>
+__device__ __forceinline__ void row_outer(const float J[8], float Dv, float H[NV][NV]) {
+  constexpr int idx[8] = {0, 1, 2, 3, 4, 5, Chain<CH>::dof6, Chain<CH>::dof7};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (idx[i] < 0) continue;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (idx[j] < 0 || idx[j] > idx[i]) continue;
+      H[idx[i]][idx[j]] += Dv * J[i] * J[j];
+    }
+  }
+}
+__device__ __forceinline__ void pyr_row(const float G[3][8], int r, float mu, float J[8]) {
+  // rows: (k=0,s=-1), (k=0,s=+1), (k=1,s=-1), (k=1,s=+1): J = Jn + s*mu*Jt_k
+  const int k = 1 + (r >> 1);
+  const float s = (r & 1) ? mu : -mu;
+#pragma unroll
+  for (int i = 0; i < 8; i++) J[i] = G[0][i] + s * G[k][i];
+}
+
+template <int CH>
+__device__ __forceinline__ float chain_mu() {
+  if constexpr (CH < 4) return MU_WHEEL;
+  else return MESH_MU[CH - 4];
+}
+
+// scalar rows (single/two-dof jacobians): 0 eq, 1..6 friction loss on dofs 6..11, 7..10 limits
+__device__ __forceinline__ void scal_dofs(int r, int& d1, float& c1, int& d2) {
+  d2 = -1;
+  if (r == 0) { d1 = EQ_DOF1; c1 = 1.0f; d2 = EQ_DOF2; }
+  else if (r <= 6) { d1 = 5 + r; c1 = 1.0f; }
+  else { d1 = LIM_DOF[(r - 7) >> 1]; c1 = ((r - 7) & 1) ? -1.0f : 1.0f; }
+}
+
+// ------------------------------------------------------------------ the per-env step
+struct Solver {
+  float M[NV][NV];           // mass matrix (lower)
+  float a0[NV];              // qacc_smooth
+  float fs[NV];              // qfrc_smooth
+};
+
+// row cost derivative bookkeeping for the line search
+__device__ __forceinline__ void ls_row(float x, float jp, float D, int type, float Rfl, float fl, float& g, float& h) {
+  if (type == 0) { g += D * x * jp; h += D * jp * jp; }
+  else if (type == 1) {
+    if (x <= -Rfl) g -= fl * jp;
+    else if (x >= Rfl) g += fl * jp;
+    else { g += D * x * jp; h += D * jp * jp; }
+  } else if (x < 0.0f) { g += D * x * jp; h += D * jp * jp; }
+}
+
+template <int CH>
+__device__ __forceinline__ void slot_loop_hess(const Slots& S, const float dirs[3][3], const float sa[2][3],
+                                               float H[NV][NV], float grad[NV]) {
+  constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
+  const float mu = chain_mu<CH>();
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const int s = s0 + k;
+    if (S.at(s, 12) == 0.0f) continue;
+    float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
+    float D = S.at(s, 3);
+    float G[3][8];
+    jac_rows<CH>(P, dirs, sa, G);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float jar = S.at(s, 4 + r);
+      if (jar < 0.0f) {
+        float J[8];
+        pyr_row(G, r, mu, J);
+        row_outer<CH>(J, D, H);
+        row_axpy<CH>(J, D * jar, grad);  // grad -= f J with f = -D jar
+      }
+    }
+  }
+}
+
+template <int CH>
+__device__ __forceinline__ void slot_loop_jp(const Slots& S, const float dirs[3][3], const float sa[2][3],
+                                             const float p[NV]) {
+  constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
+  const float mu = chain_mu<CH>();
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const int s = s0 + k;
+    if (S.at(s, 12) == 0.0f) continue;
+    float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
+    float G[3][8];
+    jac_rows<CH>(P, dirs, sa, G);
+    float gn = row_dot<CH>(G[0], p), g1 = row_dot<CH>(G[1], p), g2 = row_dot<CH>(G[2], p);
+    S.at(s, 8) = gn - mu * g1;
+    S.at(s, 9) = gn + mu * g1;
+    S.at(s, 10) = gn - mu * g2;
+    S.at(s, 11) = gn + mu * g2;
+  }
+}
+
+// jar init: jar = J a - aref, with aref = -B (J u) - K imp pos
+template <int CH>
+__device__ __forceinline__ void slot_loop_init(const Slots& S, const float dirs[3][3], const float sa[2][3],
+                                               const float a[NV], const float u[NV], float K, float B) {
+  constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
+  const float mu = chain_mu<CH>();
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const int s = s0 + k;
+    if (S.at(s, 12) == 0.0f) continue;
+    float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
+    float dist = S.at(s, 3);  // holds dist until replaced by D
+    float G[3][8];
+    jac_rows<CH>(P, dirs, sa, G);
+    float an = row_dot<CH>(G[0], a), a1 = row_dot<CH>(G[1], a), a2 = row_dot<CH>(G[2], a);
+    float vn = row_dot<CH>(G[0], u), v1 = row_dot<CH>(G[1], u), v2 = row_dot<CH>(G[2], u);
+    float imp = impedance(dist);
+    float ja[4] = {an - mu * a1, an + mu * a1, an - mu * a2, an + mu * a2};
+    float jv[4] = {vn - mu * v1, vn + mu * v1, vn - mu * v2, vn + mu * v2};
+#pragma unroll
+    for (int r = 0; r < 4; r++) S.at(s, 4 + r) = ja[r] + B * jv[r] + K * imp * dist;
+    // pyramidal regulariser shared by the 4 edges:
+    // R = (1-imp)/imp * tran*(1+mu^2) * 2 mu^2 / impratio   (see oracle make_constraint)
+    float tran = CH < 4 ? W_TRAN[CH < 4 ? CH : 0] : MESH_TRAN[CH >= 4 ? CH - 4 : 0];
+    float Rr = fmaxf(MINVAL, (1.0f - imp) / imp * tran * (1.0f + mu * mu) * (2.0f * mu * mu / IMPRATIO));
+    S.at(s, 3) = 1.0f / Rr;
+  }
+}
+
+// constraint force accumulation qfrc_c += J^T f at the current jar
+template <int CH>
+__device__ __forceinline__ void slot_loop_force(const Slots& S, const float dirs[3][3], const float sa[2][3],
+                                                float fc[NV]) {
+  constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
+  const float mu = chain_mu<CH>();
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const int s = s0 + k;
+    if (S.at(s, 12) == 0.0f) continue;
+    float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
+    float D = S.at(s, 3);
+    float G[3][8];
+    jac_rows<CH>(P, dirs, sa, G);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float jar = S.at(s, 4 + r);
+      if (jar < 0.0f) {
+        float J[8];
+        pyr_row(G, r, mu, J);
+        row_axpy<CH>(J, -D * jar, fc);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void slot_deactivate_all(const Slots& S) {
+#pragma unroll
+  for (int s = 0; s < NSLOT; s++) S.at(s, 12) = 0.0f;
+}
+
+// plane-cylinder for wheel W: writes up to 4 slots (mjc_PlaneCylinder restatement)
+template <int W>
+__device__ __forceinline__ int wheel_contacts(const Slots& S, const float p[3], const float R[9], const float cyl_b[3]) {
+  constexpr int s0 = W * 4;
+  float c[3], axis[3];
+  const float* an = W_ANCHOR[W];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    c[k] = p[k] + R[3 * k] * an[0] + R[3 * k + 1] * an[1] + R[3 * k + 2] * an[2];
+    axis[k] = R[3 * k] * cyl_b[0] + R[3 * k + 1] * cyl_b[1] + R[3 * k + 2] * cyl_b[2];
+  }
+  float prjaxis = axis[2];
+  if (prjaxis > 0) { axis[0] = -axis[0]; axis[1] = -axis[1]; axis[2] = -axis[2]; prjaxis = -prjaxis; }
+  float dist0 = c[2];
+  float vec[3] = {axis[0] * prjaxis, axis[1] * prjaxis, axis[2] * prjaxis - 1.0f};
+  float len2 = dot(vec, vec), prjvec;
+  if (len2 >= MINVAL * MINVAL) {
+    float sc = CYL_R / sqrtf(len2);
+    vec[0] *= sc; vec[1] *= sc; vec[2] *= sc;
+    prjvec = vec[2];
+  } else {  // disk parallel to the plane (measure zero): any in-plane radius
+    vec[0] = R[0] * CYL_R; vec[1] = R[3] * CYL_R; vec[2] = R[6] * CYL_R;
+    prjvec = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) axis[k] *= CYL_H;
+  prjaxis *= CYL_H;
+  int cnt = 0;
+  float dpos[4][3], dd[4];
+  bool act[4] = {false, false, false, false};
+  float d1 = dist0 + prjaxis + prjvec;
+  if (d1 <= 0.0f) {
+    act[0] = true; dd[0] = d1;
+#pragma unroll
+    for (int k = 0; k < 3; k++) dpos[0][k] = c[k] + vec[k] + axis[k];
+    float d2 = dist0 - prjaxis + prjvec;
+    if (d2 <= 0.0f) {
+      act[1] = true; dd[1] = d2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) dpos[1][k] = c[k] + vec[k] - axis[k];
+    }
+    if (dist0 + prjaxis - prjvec <= 0.0f) {
+      float v1[3];
+      cross(v1, vec, axis);
+      float nv1 = sqrtf(dot(v1, v1));
+      float sc = nv1 < MINVAL ? 0.0f : CYL_R * 0.8660254037844386f / nv1;
+      float d3 = dist0 + prjaxis - 0.5f * prjvec;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        float sg = t == 0 ? -1.0f : 1.0f;
+        act[2 + t] = true; dd[2 + t] = d3;
+#pragma unroll
+        for (int k = 0; k < 3; k++) dpos[2 + t][k] = c[k] + axis[k] - 0.5f * vec[k] + sg * sc * v1[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    // included in the constraint set only if dist < margin - gap = 0
+    bool on = act[t] && dd[t] < 0.0f;
+    S.at(s0 + t, 12) = on ? 1.0f : 0.0f;
+    if (on) {
+      // midpoint contact position, then chassis-frame point relative to the chassis origin
+      float w[3] = {dpos[t][0] - p[0], dpos[t][1] - p[1], dpos[t][2] - 0.5f * dd[t] - p[2]};
+      S.at(s0 + t, 0) = R[0] * w[0] + R[3] * w[1] + R[6] * w[2];
+      S.at(s0 + t, 1) = R[1] * w[0] + R[4] * w[1] + R[7] * w[2];
+      S.at(s0 + t, 2) = R[2] * w[0] + R[5] * w[1] + R[8] * w[2];
+      S.at(s0 + t, 3) = dd[t];
+      cnt++;
+    }
+  }
+  return cnt;
+}
+
+// plane vs convex hull of welded mesh K: support vertex + up to 3 spread vertices
+template <int K>
+__device__ __forceinline__ int mesh_contacts(const Slots& S, const float p[3], const float R[9]) {
+  constexpr int s0 = 16 + K * 4;
+#pragma unroll
+  for (int t = 0; t < 4; t++) S.at(s0 + t, 12) = 0.0f;
+  // conservative lower bound on the hull's height (chassis-frame AABB)
+  float zc = p[2], ext = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float cen = 0.5f * (HULL_LO[K][k] + HULL_HI[K][k]), half = 0.5f * (HULL_HI[K][k] - HULL_LO[K][k]);
+    zc += R[6 + k] * cen;
+    ext += fabsf(R[6 + k]) * half;
+  }
+  if (zc - ext > 0.0f) return 0;
+  int best = 0;
+  float bz = 3.0e38f;
+  for (int i = 0; i < HULL_N[K]; i++) {
+    float z = p[2] + R[6] * HULL[K][i][0] + R[7] * HULL[K][i][1] + R[8] * HULL[K][i][2];
+    if (z < bz) { bz = z; best = i; }
+  }
+  if (bz > 0.0f) return 0;
+  int sel[4] = {best, -1, -1, -1};
+  int nsel = 1;
+  for (int it = 0; it < 3; it++) {
+    int pick = -1;
+    float pickd = 1e-12f;
+    for (int i = 0; i < HULL_N[K]; i++) {
+      float z = p[2] + R[6] * HULL[K][i][0] + R[7] * HULL[K][i][1] + R[8] * HULL[K][i][2];
+      if (z > 0.0f) continue;
+      float dmin = 3.0e38f;
+      for (int s = 0; s < nsel; s++) {
+        float e0 = HULL[K][i][0] - HULL[K][sel[s]][0], e1 = HULL[K][i][1] - HULL[K][sel[s]][1],
+              e2 = HULL[K][i][2] - HULL[K][sel[s]][2];
+        dmin = fminf(dmin, e0 * e0 + e1 * e1 + e2 * e2);
+      }
+      if (dmin > pickd) { pickd = dmin; pick = i; }
+    }
+    if (pick < 0) break;
+    sel[nsel++] = pick;
+  }
+  int cnt = 0;
+  for (int t = 0; t < nsel; t++) {
+    int i = sel[t];
+    float z = p[2] + R[6] * HULL[K][i][0] + R[7] * HULL[K][i][1] + R[8] * HULL[K][i][2];
+    if (!(z < 0.0f)) continue;
+    // P_b = h - n_b*dist/2, n_b = R^T e_z
+    S.at(s0 + t, 0) = HULL[K][i][0] - R[6] * 0.5f * z;
+    S.at(s0 + t, 1) = HULL[K][i][1] - R[7] * 0.5f * z;
+    S.at(s0 + t, 2) = HULL[K][i][2] - R[8] * 0.5f * z;
+    S.at(s0 + t, 3) = z;
+    S.at(s0 + t, 12) = 1.0f;
+    cnt++;
+  }
+  return cnt;
+}
+
+#define FOR_CHAINS(F, ...) \
+  F<0>(__VA_ARGS__);       \
+  F<1>(__VA_ARGS__);       \
+  F<2>(__VA_ARGS__);       \
+  F<3>(__VA_ARGS__);       \
+  F<4>(__VA_ARGS__);       \
+  F<5>(__VA_ARGS__)
+
+struct StepResult {
+  float qacc[NV];  // u coords
+  float acce[NV];  // implicit-damping Euler acceleration, u coords
+  bool bad;
+};
+
+// forward dynamics + constraint solve for one env (state in registers), u coordinates
+__device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
+                         const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
+  // front steer angles -> spin / cylinder axes in the chassis frame
+  float sa[2][3], cyl[2][3];
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    float d = qpos[W_STEER_QPOS[2 + s]];
+    float c = cosf(d), sn = sinf(d);
+    rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
+    rot_axis(cyl[s], S_AXIS[s], W_CYL_AXIS[2 + s], c, sn);
+  }
+  Solver sv;
+  build_M(sv.M, sa);
+  float b[NV];
+  bias(u, R, sa, b);
+  // passive damping + actuators (mj_passive, mj_fwdActuation)
+#pragma unroll
+  for (int i = 0; i < NV; i++) sv.fs[i] = -b[i] - DAMPING[i] * u[i];
+  {
+    float c0 = ctrl[0];
+    if (ACT_CTRLLIMITED[0]) c0 = fminf(fmaxf(c0, ACT_CTRLRANGE[0][0]), ACT_CTRLRANGE[0][1]);
+    float f0 = ACT_GAIN[0] * c0 + ACT_BIAS1[0] * qpos[ACT_STEER_QPOS] + ACT_BIAS2[0] * u[ACT_STEER_DOF];
+    if (ACT_FORCELIMITED[0]) f0 = fminf(fmaxf(f0, ACT_FORCERANGE[0][0]), ACT_FORCERANGE[0][1]);
+    sv.fs[ACT_STEER_DOF] += f0;
+    float c1 = ctrl[1], c2 = ctrl[2];
+    if (ACT_CTRLLIMITED[1]) c1 = fminf(fmaxf(c1, ACT_CTRLRANGE[1][0]), ACT_CTRLRANGE[1][1]);
+    if (ACT_CTRLLIMITED[2]) c2 = fminf(fmaxf(c2, ACT_CTRLRANGE[2][0]), ACT_CTRLRANGE[2][1]);
+    float f1 = ACT_GAIN[1] * c1 + ACT_BIAS2[1] * u[ACT_RL_DOF];
+    float f2 = ACT_GAIN[2] * c2 + ACT_BIAS2[2] * u[ACT_RR_DOF];
+    if (ACT_FORCELIMITED[1]) f1 = fminf(fmaxf(f1, ACT_FORCERANGE[1][0]), ACT_FORCERANGE[1][1]);
+    if (ACT_FORCELIMITED[2]) f2 = fminf(fmaxf(f2, ACT_FORCERANGE[2][0]), ACT_FORCERANGE[2][1]);
+    sv.fs[ACT_RL_DOF] += f1;
+    sv.fs[ACT_RR_DOF] += f2;
+  }
+  // qacc_smooth = M^-1 fs
+  float L[NV][NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < NV; j++) L[i][j] = sv.M[i][j];
+  chol12(L);
+#pragma unroll
+  for (int i = 0; i < NV; i++) sv.a0[i] = sv.fs[i];
+  chol12_solve(L, sv.a0);
+
+  // contacts
+  if (flags & F_CONTACTS) {
+    const float rear_cyl[3] = {W_CYL_AXIS[0][0], W_CYL_AXIS[0][1], W_CYL_AXIS[0][2]};
+    const float rear_cyl1[3] = {W_CYL_AXIS[1][0], W_CYL_AXIS[1][1], W_CYL_AXIS[1][2]};
+    wheel_contacts<0>(S, qpos, R, rear_cyl);
+    wheel_contacts<1>(S, qpos, R, rear_cyl1);
+    wheel_contacts<2>(S, qpos, R, cyl[0]);
+    wheel_contacts<3>(S, qpos, R, cyl[1]);
+    mesh_contacts<0>(S, qpos, R);
+    mesh_contacts<1>(S, qpos, R);
+  } else {
+    slot_deactivate_all(S);
+  }
+  // contact frame directions in the chassis frame: n = e_z, t1 = e_y, t2 = -e_x (mju_makeFrame)
+  float dirs[3][3] = {{R[6], R[7], R[8]}, {R[3], R[4], R[5]}, {-R[0], -R[1], -R[2]}};
+
+  float K, B;
+  ref_kb(K, B);
+  // scalar rows: jar, D, type, R*floss
+  float sj[NSCAL], sD[NSCAL], sRfl[NSCAL], sfl[NSCAL], sjp[NSCAL];
+  bool sact[NSCAL];
+  float eqc2;
+  {
+    // equality (polycoef), pos and diagApprox
+    float dif = qpos[EQ_QPOS2] - QPOS0[EQ_QPOS2];
+    float cpos = EQ_POLY[0] + dif * (EQ_POLY[1] + dif * (EQ_POLY[2] + dif * (EQ_POLY[3] + dif * EQ_POLY[4])));
+    float cvel = EQ_POLY[1] + dif * (2 * EQ_POLY[2] + dif * (3 * EQ_POLY[3] + dif * 4 * EQ_POLY[4]));
+    eqc2 = -cvel;
+    float pos = qpos[EQ_QPOS1] - QPOS0[EQ_QPOS1] - cpos;
+    float imp = impedance(pos);
+    float diag = DOF_INVW[EQ_DOF1] + DOF_INVW[EQ_DOF2];
+    float Rr = fmaxf(MINVAL, (1 - imp) / imp * diag);
+    sD[0] = 1.0f / Rr; sRfl[0] = 0; sfl[0] = 0; sact[0] = true;
+    float ja = warm_u[EQ_DOF1] + eqc2 * warm_u[EQ_DOF2];
+    float jv = u[EQ_DOF1] + eqc2 * u[EQ_DOF2];
+    sj[0] = -B * jv - K * imp * pos;  // holds aref for now
+    (void)ja;
+  }
+#pragma unroll
+  for (int r = 1; r <= 6; r++) {
+    int d = 5 + r;
+    float imp = impedance(0.0f);
+    float Rr = fmaxf(MINVAL, (1 - imp) / imp * DOF_INVW[d]);
+    sD[r] = 1.0f / Rr; sfl[r] = FRICTIONLOSS[d]; sRfl[r] = Rr * FRICTIONLOSS[d];
+    sact[r] = FRICTIONLOSS[d] > 0.0f;
+    sj[r] = -B * u[d];
+  }
+#pragma unroll
+  for (int r = 7; r < NSCAL; r++) {
+    int l = (r - 7) >> 1, side = ((r - 7) & 1) ? 1 : -1;
+    float q = qpos[LIM_QPOS[l]];
+    float dist = side * (LIM_RANGE[l][side > 0 ? 1 : 0] - q);
+    sact[r] = dist < 0.0f;
+    float imp = impedance(dist);
+    float Rr = fmaxf(MINVAL, (1 - imp) / imp * DOF_INVW[LIM_DOF[l]]);
+    sD[r] = 1.0f / Rr; sfl[r] = 0; sRfl[r] = 0;
+    float jv = -side * u[LIM_DOF[l]];
+    sj[r] = -B * jv - K * imp * dist;
+  }
+  // aref of scalar rows is in sj; jar(a) = J a - aref
+
+  // warmstart: the cheaper of qacc_warmstart and qacc_smooth (cost = gauss + constraint)
+  auto scal_J_dot = [&](int r, const float x[NV]) -> float {
+    if (r == 0) return x[EQ_DOF1] + eqc2 * x[EQ_DOF2];
+    if (r <= 6) return x[5 + r];
+    int l = (r - 7) >> 1;
+    float c = ((r - 7) & 1) ? -1.0f : 1.0f;
+    return c * x[LIM_DOF[l]];
+  };
+  auto scal_cost = [&](int r, float x) -> float {
+    if (!sact[r]) return 0.0f;
+    if (r == 0) return 0.5f * sD[r] * x * x;
+    if (r <= 6) {
+      if (x <= -sRfl[r]) return -sfl[r] * x - 0.5f * sRfl[r] * sfl[r];
+      if (x >= sRfl[r]) return sfl[r] * x - 0.5f * sRfl[r] * sfl[r];
+      return 0.5f * sD[r] * x * x;
+    }
+    return x < 0.0f ? 0.5f * sD[r] * x * x : 0.0f;
+  };
+  float cost_w = 0.0f, cost_s = 0.0f;
+  {
+    float dw[NV], Mdw[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) dw[i] = warm_u[i] - sv.a0[i];
+    symv12(sv.M, dw, Mdw);
+#pragma unroll
+    for (int i = 0; i < NV; i++) cost_w += 0.5f * dw[i] * Mdw[i];
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      cost_w += scal_cost(r, scal_J_dot(r, warm_u) - sj[r]);
+      cost_s += scal_cost(r, scal_J_dot(r, sv.a0) - sj[r]);
+    }
+  }
+  // contact rows: need jar at both candidates. Initialise slots at warm and at a0 (cheap).
+  // slot field 4..7 temporarily = J a_w - aref ; we evaluate cost then re-init for the chosen.
+  FOR_CHAINS(slot_loop_init, S, dirs, sa, warm_u, u, K, B);
+  float cw_c = 0.0f;
+#pragma unroll 1
+  for (int s = 0; s < NSLOT; s++) {
+    if (S.at(s, 12) == 0.0f) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float x = S.at(s, 4 + r);
+      if (x < 0.0f) cw_c += 0.5f * S.at(s, 3) * x * x;
+    }
+  }
+  cost_w += cw_c;
+  // jar at a0 = jar_w + J (a0 - warm): use the Jp machinery with p = a0 - warm
+  float a[NV];
+  {
+    float dpa[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) dpa[i] = sv.a0[i] - warm_u[i];
+    FOR_CHAINS(slot_loop_jp, S, dirs, sa, dpa);
+    float cs_c = 0.0f;
+#pragma unroll 1
+    for (int s = 0; s < NSLOT; s++) {
+      if (S.at(s, 12) == 0.0f) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float x = S.at(s, 4 + r) + S.at(s, 8 + r);
+        if (x < 0.0f) cs_c += 0.5f * S.at(s, 3) * x * x;
+      }
+    }
+    cost_s += cs_c;
+    bool use_w = cost_w < cost_s;
+#pragma unroll
+    for (int i = 0; i < NV; i++) a[i] = use_w ? warm_u[i] : sv.a0[i];
+    if (!use_w) {
+#pragma unroll 1
+      for (int s = 0; s < NSLOT; s++) {
+        if (S.at(s, 12) == 0.0f) continue;
+#pragma unroll
+        for (int r = 0; r < 4; r++) S.at(s, 4 + r) += S.at(s, 8 + r);
+      }
+    }
+  }
+  // scalar jar at a
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
+
+  // ---------------- Newton iterations
+  const float scale = 1.0f / (MEANINERTIA * (float)NV);
+  bool done = false;
+#pragma unroll 1
+  for (int it = 0; it < MAXIT; it++) {
+    if (done) break;
+    float H[NV][NV], grad[NV];
+    {
+      float da[NV];
+#pragma unroll
+      for (int i = 0; i < NV; i++) da[i] = a[i] - sv.a0[i];
+      symv12(sv.M, da, grad);
+    }
+#pragma unroll
+    for (int i = 0; i < NV; i++)
+#pragma unroll
+      for (int j = 0; j < NV; j++) H[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
+    // scalar rows
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      if (!sact[r]) continue;
+      int d1, d2;
+      float c1;
+      scal_dofs(r, d1, c1, d2);
+      float x = sj[r];
+      float f;
+      bool quad;
+      if (r == 0) { f = -sD[r] * x; quad = true; }
+      else if (r <= 6) {
+        if (x <= -sRfl[r]) { f = sfl[r]; quad = false; }
+        else if (x >= sRfl[r]) { f = -sfl[r]; quad = false; }
+        else { f = -sD[r] * x; quad = true; }
+      } else { quad = x < 0.0f; f = quad ? -sD[r] * x : 0.0f; }
+      grad[d1] -= f * c1;
+      if (d2 >= 0) grad[d2] -= f * eqc2;
+      if (quad) {
+        H[d1][d1] += sD[r] * c1 * c1;
+        if (d2 >= 0) {
+          H[d2][d2] += sD[r] * eqc2 * eqc2;
+          if (d2 > d1) H[d2][d1] += sD[r] * c1 * eqc2;
+          else H[d1][d2] += sD[r] * c1 * eqc2;
+        }
+      }
+    }
+    FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad);
+    float gn2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) gn2 += grad[i] * grad[i];
+    if (scale * sqrtf(gn2) < 1e-10f) break;
+    chol12(H);
+    float pdir[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
+    chol12_solve(H, pdir);
+    // Jp for all rows
+    FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir);
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) sjp[r] = scal_J_dot(r, pdir);
+    // exact line search on the piecewise-linear derivative phi'(alpha)
+    float Mp[NV];
+    symv12(sv.M, pdir, Mp);
+    float pMp = 0.0f, pg0 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { pMp += pdir[i] * Mp[i]; pg0 += Mp[i] * (a[i] - sv.a0[i]); }
+    auto dphi = [&](float al, float& g, float& h) {
+      g = pg0 + al * pMp;
+      h = pMp;
+#pragma unroll
+      for (int r = 0; r < NSCAL; r++) {
+        if (!sact[r]) continue;
+        int type = r == 0 ? 0 : (r <= 6 ? 1 : 2);
+        ls_row(sj[r] + al * sjp[r], sjp[r], sD[r], type, sRfl[r], sfl[r], g, h);
+      }
+#pragma unroll 1
+      for (int s = 0; s < NSLOT; s++) {
+        if (S.at(s, 12) == 0.0f) continue;
+        float D = S.at(s, 3);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          float jp = S.at(s, 8 + r);
+          float x = S.at(s, 4 + r) + al * jp;
+          if (x < 0.0f) { g += D * x * jp; h += D * jp * jp; }
+        }
+      }
+    };
+    float g0, h0;
+    dphi(0.0f, g0, h0);
+    if (!(g0 < 0.0f)) break;  // no descent
+    float lo = 0.0f, hi = 3.0e38f, al = 1.0f;
+#pragma unroll 1
+    for (int k = 0; k < LSIT; k++) {
+      float g, h;
+      dphi(al, g, h);
+      if (fabsf(g) <= 1e-6f * fabsf(g0)) break;
+      if (g < 0.0f) lo = al; else hi = al;
+      float nal = al - g / h;
+      if (!(nal > lo && nal < hi)) nal = (hi < 3.0e38f) ? 0.5f * (lo + hi) : 2.0f * al;
+      al = nal;
+    }
+    // move, count row-state changes (no change at a full Newton step = converged)
+    int changed = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) a[i] += al * pdir[i];
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      float x0 = sj[r], x1 = sj[r] + al * sjp[r];
+      if (sact[r] && r > 0) {
+        if (r <= 6) changed += ((x0 <= -sRfl[r]) != (x1 <= -sRfl[r])) + ((x0 >= sRfl[r]) != (x1 >= sRfl[r]));
+        else changed += (x0 < 0.0f) != (x1 < 0.0f);
+      }
+      sj[r] = x1;
+    }
+#pragma unroll 1
+    for (int s = 0; s < NSLOT; s++) {
+      if (S.at(s, 12) == 0.0f) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float x0 = S.at(s, 4 + r), x1 = x0 + al * S.at(s, 8 + r);
+        changed += (x0 < 0.0f) != (x1 < 0.0f);
+        S.at(s, 4 + r) = x1;
+      }
+    }
+    if (changed == 0 && fabsf(al - 1.0f) < 1e-3f) done = true;
+  }
+#pragma unroll
+  for (int i = 0; i < NV; i++) out.qacc[i] = a[i];
+  // qfrc_constraint = J^T f at the solution
+  float fc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) fc[i] = 0.0f;
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++) {
+    if (!sact[r]) continue;
+    int d1, d2;
+    float c1;
+    scal_dofs(r, d1, c1, d2);
+    float x = sj[r], f;
+    if (r == 0) f = -sD[r] * x;
+    else if (r <= 6) f = (x <= -sRfl[r]) ? sfl[r] : ((x >= sRfl[r]) ? -sfl[r] : -sD[r] * x);
+    else f = x < 0.0f ? -sD[r] * x : 0.0f;
+    fc[d1] += f * c1;
+    if (d2 >= 0) fc[d2] += f * eqc2;
+  }
+  FOR_CHAINS(slot_loop_force, S, dirs, sa, fc);
+  // implicit damping Euler: (M + h diag(B)) acc = fs + fc
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < NV; j++) L[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
+#pragma unroll
+  for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
+  chol12(L);
+#pragma unroll
+  for (int i = 0; i < NV; i++) out.acce[i] = sv.fs[i] + fc[i];
+  chol12_solve(L, out.acce);
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < NV; i++) bad |= is_bad(a[i]);
+  out.bad = bad;
+}
+
+// ------------------------------------------------------------------ state I/O helpers
+__device__ __forceinline__ void reset_pose(float qpos[13], float qvel[NV], float warm[NV]) {
+  // SimpleMapSpawner.load_random_environment: qpos0 with chassis at (0,0,0.1), identity quat
+#pragma unroll
+  for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+  qpos[0] = 0.0f; qpos[1] = 0.0f; qpos[2] = 0.1f;
+  qpos[3] = 1.0f; qpos[4] = 0.0f; qpos[5] = 0.0f; qpos[6] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
+}
+
+__device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_t episode, float& gx, float& gy) {
+  uint32_t c[4] = {(uint32_t)genv, episode, 0u, 0u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float d = 2.0f + 6.0f * u01(c[0]);
+  float th = 6.283185307179586f * u01(c[1]);
+  gx = d * cosf(th);
+  gy = d * sinf(th);
+}
+
+// reset env e: writes state words + observation
+__device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode) {
+  float qpos[13], qvel[NV], warm[NV];
+  reset_pose(qpos, qvel, warm);
+  float gx, gy;
+  goal_sample(seed, genv, episode, gx, gy);
+  float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+  normq(q);
+  float R[9];
+  quat_R(q, R);
+  float ref[3] = {qpos[0], qpos[1], qpos[2]};  // odometry reference = chassis xpos at reset
+#pragma unroll
+  for (int i = 0; i < 13; i++) state[(size_t)(ST_QPOS + i) * n + e] = qpos[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    state[(size_t)(ST_QVEL + i) * n + e] = 0.0f;
+    state[(size_t)(ST_WARM + i) * n + e] = 0.0f;
+  }
+  state[(size_t)ST_GOAL * n + e] = gx;
+  state[(size_t)(ST_GOAL + 1) * n + e] = gy;
+#pragma unroll
+  for (int k = 0; k < 3; k++) state[(size_t)(ST_REF + k) * n + e] = ref[k];
+  state[(size_t)ST_STEP * n + e] = __uint_as_float(0u);
+  state[(size_t)ST_EPIS * n + e] = __uint_as_float(episode);
+  observe(qpos, q, R, gx, gy, ref, obs + e, n);
+}
+
+}  // namespace ak
+
+// ====================================================================== kernels
+using namespace ak;
+
+extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) {
+  __shared__ float lds[NSLOT * NF * 64];
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * 64 + lane;
+  if (e >= A.n) return;
+  const int n = A.n;
+  Slots S{lds + lane};
+  float* st = A.state;
+  float qpos[13], qvel[NV], warm[NV];
+#pragma unroll
+  for (int i = 0; i < 13; i++) qpos[i] = st[(size_t)(ST_QPOS + i) * n + e];
+#pragma unroll
+  for (int i = 0; i < NV; i++) qvel[i] = st[(size_t)(ST_QVEL + i) * n + e];
+#pragma unroll
+  for (int i = 0; i < NV; i++) warm[i] = st[(size_t)(ST_WARM + i) * n + e];
+  const float gx = st[(size_t)ST_GOAL * n + e], gy = st[(size_t)(ST_GOAL + 1) * n + e];
+  const float ref[3] = {st[(size_t)ST_REF * n + e], st[(size_t)(ST_REF + 1) * n + e], st[(size_t)(ST_REF + 2) * n + e]};
+  uint32_t step = __float_as_uint(st[(size_t)ST_STEP * n + e]);
+  uint32_t episode = __float_as_uint(st[(size_t)ST_EPIS * n + e]);
+  const float a0 = A.action[2 * (size_t)e], a1 = A.action[2 * (size_t)e + 1];
+
+  // controller -> ctrl (float64, reference thresholds)
+  float ctrl[3];
+  bool badctrl;
+  controller(a0, a1, ctrl, badctrl);
+
+  // mj_checkPos / mj_checkVel: bad state -> mj_resetData (qpos0, zero velocity/warmstart/ctrl)
+  bool bad_state = false;
+#pragma unroll
+  for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
+#pragma unroll
+  for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
+  for (int pass = 0; pass < 2; pass++) {
+    if (bad_state) {
+#pragma unroll
+      for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+#pragma unroll
+      for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
+      ctrl[0] = ctrl[1] = ctrl[2] = 0.0f;
+    }
+    // kinematics (pre-integration)
+    float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+    normq(q);
+    float R[9];
+    quat_R(q, R);
+    // u = (R^T v, w, hinges)
+    float u[NV], wu[NV];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      u[k] = R[k] * qvel[0] + R[3 + k] * qvel[1] + R[6 + k] * qvel[2];
+      wu[k] = R[k] * warm[0] + R[3 + k] * warm[1] + R[6 + k] * warm[2];
+    }
+#pragma unroll
+    for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
+    StepResult res;
+    dynamics(S, qpos, u, wu, R, ctrl, A.flags, res);
+    if (res.bad && pass == 0) { bad_state = true; continue; }
+
+    // observation / reward on the pre-integration pose
+    const uint32_t nstep = step + 1;
+    const bool trunc = nstep >= (uint32_t)MAX_STEPS;
+    float head[7];
+    ObsOut oh = observe_head(qpos, q, R, gx, gy, ref, head);
+    const bool done_pre = oh.term || trunc;
+    const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
+    float* dst = (autoreset && A.tobs) ? A.tobs + e : A.obs + e;
+    ObsOut o = observe(qpos, q, R, gx, gy, ref, dst, n);
+    A.reward[e] = o.reward;
+    A.term[e] = o.term ? 1 : 0;
+    A.trunc[e] = trunc ? 1 : 0;
+    if (A.info) {
+      A.info[e] = o.minl;
+      A.info[(size_t)n + e] = o.coll ? 1.0f : 0.0f;
+      A.info[2 * (size_t)n + e] = o.dist;
+      A.info[3 * (size_t)n + e] = bad_state ? 1.0f : 0.0f;
+    }
+
+    if (autoreset) {
+      reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1);
+      return;
+    }
+    // mj_Euler: qvel += h acc (u coords -> world linear), integrate positions
+    float vb[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) vb[k] = u[k] + DT * res.acce[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) qvel[k] = R[3 * k] * vb[0] + R[3 * k + 1] * vb[1] + R[3 * k + 2] * vb[2];
+#pragma unroll
+    for (int i = 3; i < NV; i++) qvel[i] = u[i] + DT * res.acce[i];
+#pragma unroll
+    for (int k = 0; k < 3; k++) qpos[k] += DT * qvel[k];
+    {
+      float w[3] = {qvel[3], qvel[4], qvel[5]};
+      float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      float ang = DT * wn;
+      float ax[3];
+      if (wn < MINVAL) { ax[0] = 1; ax[1] = 0; ax[2] = 0; ang = 0; }
+      else { ax[0] = w[0] / wn; ax[1] = w[1] / wn; ax[2] = w[2] / wn; }
+      float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+      float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
+      float qq[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+      normq(qq);
+      qpos[3] = qq[0] * qr[0] - qq[1] * qr[1] - qq[2] * qr[2] - qq[3] * qr[3];
+      qpos[4] = qq[0] * qr[1] + qq[1] * qr[0] + qq[2] * qr[3] - qq[3] * qr[2];
+      qpos[5] = qq[0] * qr[2] - qq[1] * qr[3] + qq[2] * qr[0] + qq[3] * qr[1];
+      qpos[6] = qq[0] * qr[3] + qq[1] * qr[2] - qq[2] * qr[1] + qq[3] * qr[0];
+    }
+#pragma unroll
+    for (int j = 7; j < 13; j++) qpos[j] += DT * qvel[j - 1];
+    // qacc_warmstart <- qacc (back to q coords)
+#pragma unroll
+    for (int k = 0; k < 3; k++) warm[k] = R[3 * k] * res.qacc[0] + R[3 * k + 1] * res.qacc[1] + R[3 * k + 2] * res.qacc[2];
+#pragma unroll
+    for (int i = 3; i < NV; i++) warm[i] = res.qacc[i];
+#pragma unroll
+    for (int i = 0; i < 13; i++) st[(size_t)(ST_QPOS + i) * n + e] = qpos[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) st[(size_t)(ST_QVEL + i) * n + e] = qvel[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) st[(size_t)(ST_WARM + i) * n + e] = warm[i];
+    st[(size_t)ST_STEP * n + e] = __uint_as_float(nstep);
+    return;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256) ackphys_reset_kernel(const uint8_t* mask, float* state, float* obs,
+                                                                       int n, uint64_t seed, int64_t env_offset) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  if (mask && !mask[e]) return;
+  uint32_t episode = __float_as_uint(state[(size_t)ST_EPIS * n + e]) + 1u;
+  reset_env(state, obs, n, e, seed, env_offset + e, episode);
+}
+
+extern "C" __global__ void __launch_bounds__(256) ackphys_actions_kernel(float* actions, int n, int k_steps,
+                                                                         uint64_t seed, uint32_t step0, int64_t env_offset) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  for (int k = 0; k < k_steps; k++) {
+    uint32_t c[4] = {(uint32_t)(env_offset + e), step0 + (uint32_t)k, 1u, 0u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float2 v = make_float2(2.0f * u01(c[0]) - 1.0f, 2.0f * u01(c[1]) - 1.0f);
+    reinterpret_cast<float2*>(actions)[(size_t)k * n + e] = v;
+  }
+}
+
+// ====================================================================== C-ABI (include/ackphys.h)
+#include "../../include/ackphys.h"
+#include "../../include/ackphys_model.h"
+#include <stdio.h>
+#include <string.h>
+
+struct ackphys_ctx {
+  int n_env;
+  int device;
+  int64_t env_offset;
+};
+
+static thread_local char g_err[512];
+static int fail(int code, const char* msg) {
+  snprintf(g_err, sizeof g_err, "%s", msg);
+  return code;
+}
+static int hipfail(hipError_t e, const char* where) {
+  snprintf(g_err, sizeof g_err, "%s: %s", where, hipGetErrorString(e));
+  return ACKPHYS_EHIP;
+}
+
+static uint64_t fnv1a64(const unsigned char* p, size_t n) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 0x100000001B3ull; }
+  return h;
+}
+
+extern "C" {
+
+const char* ackphys_last_error(void) { return g_err; }
+const char* ackphys_version(void) { return "ackphys 0.1 (gfx950, lane-per-env)"; }
+uint64_t ackphys_model_fnv(void) { return apg::MODEL_FNV; }
+
+int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device, ackphys_t** out) {
+  if (!out) return fail(ACKPHYS_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!model_blob || nbytes < sizeof(apm_model_t)) return fail(ACKPHYS_EMODEL, "model blob missing or too small");
+  const apm_model_t* m = (const apm_model_t*)model_blob;
+  if (m->magic != APM_MAGIC || m->version != APM_VERSION || m->nbytes != nbytes)
+    return fail(ACKPHYS_EMODEL, "model blob: bad magic/version/size");
+  if (fnv1a64((const unsigned char*)model_blob, nbytes) != apg::MODEL_FNV)
+    return fail(ACKPHYS_EMODEL, "model blob does not match the model these kernels were specialised on "
+                                "(regenerate with python -m mujoco_playground_amd.model.build and rebuild)");
+  if (n_env <= 0) return fail(ACKPHYS_EINVAL, "n_env must be positive");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hipfail(e, "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return fail(ACKPHYS_EINVAL, "device index out of range");
+  ackphys_ctx* c = new ackphys_ctx;
+  c->n_env = n_env;
+  c->device = device;
+  c->env_offset = 0;
+  *out = c;
+  return ACKPHYS_OK;
+}
+
+int ackphys_destroy(ackphys_t* ctx) {
+  delete ctx;
+  return ACKPHYS_OK;
+}
+
+int ackphys_set_env_offset(ackphys_t* ctx, int64_t off) {
+  if (!ctx) return fail(ACKPHYS_EINVAL, "ctx is NULL");
+  ctx->env_offset = off;
+  return ACKPHYS_OK;
+}
+
+int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, float* reward, uint8_t* term,
+                 uint8_t* trunc, float* terminal_obs, float* info, uint32_t flags, uint64_t seed, void* stream) {
+  if (!ctx || !action || !state || !obs || !reward || !term || !trunc)
+    return fail(ACKPHYS_EINVAL, "ackphys_step: NULL argument");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, ctx->n_env, flags, seed, ctx->env_offset};
+  int blocks = (ctx->n_env + 63) / 64;
+  hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");
+  return ACKPHYS_OK;
+}
+
+int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* state, float* obs, void* stream) {
+  if (!ctx || !state || !obs) return fail(ACKPHYS_EINVAL, "ackphys_reset: NULL argument");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  int blocks = (ctx->n_env + 255) / 256;
+  hipLaunchKernelGGL(ackphys_reset_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
+                     ctx->n_env, seed, ctx->env_offset);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hipfail(e, "ackphys_reset_kernel launch");
+  return ACKPHYS_OK;
+}
+
+int ackphys_random_actions(ackphys_t* ctx, float* actions, int k_steps, uint64_t seed, uint32_t step0, void* stream) {
+  if (!ctx || !actions || k_steps <= 0) return fail(ACKPHYS_EINVAL, "ackphys_random_actions: bad argument");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  int blocks = (ctx->n_env + 255) / 256;
+  hipLaunchKernelGGL(ackphys_actions_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, actions, ctx->n_env,
+                     k_steps, seed, step0, ctx->env_offset);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hipfail(e, "ackphys_actions_kernel launch");
+  return ACKPHYS_OK;
+}
+
+}  // extern "C"

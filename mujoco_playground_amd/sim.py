@@ -1,0 +1,101 @@
+"""BatchedAckermannSim: device-resident state for N Ackermann-robot envs + the HIP step.
+
+Torch tensors are only the device array container; every byte of physics is computed by
+libackphys.so (include/ackphys.h). This is the batched replacement for the reference's
+`mujoco.MjData` + `mujoco.mj_step` pair (src/rl/envs/ackermann_env.py:150-153, :200).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+NSTATE, NOBS = 44, 79
+CONTACTS, AUTORESET = 1, 2
+
+# state word offsets (include/ackphys.h)
+ST_QPOS, ST_QVEL, ST_WARM, ST_GOAL, ST_REF, ST_STEP, ST_EPIS = 0, 13, 25, 37, 39, 42, 43
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class BatchedAckermannSim:
+    def __init__(self, num_envs: int, device="cuda:0", seed: int = 0, contacts: bool = True,
+                 env_offset: int = 0, model_blob: bytes | None = None):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
+        self.n = int(num_envs)
+        self.seed = int(seed)
+        self.contacts = bool(contacts)
+        L = _lib.lib()
+        blob = model_blob if model_blob is not None else _lib.load_blob()
+        ctx = C.c_void_p()
+        _lib.check(L.ackphys_create(blob, len(blob), self.n, self.device.index or 0, C.byref(ctx)), "ackphys_create")
+        self._ctx = ctx
+        _lib.check(L.ackphys_set_env_offset(ctx, int(env_offset)), "ackphys_set_env_offset")
+        f32, u8 = torch.float32, torch.uint8
+        d = self.device
+        self.state = torch.zeros(NSTATE, self.n, dtype=f32, device=d)
+        self.obs_soa = torch.zeros(NOBS, self.n, dtype=f32, device=d)
+        self.terminal_obs_soa = torch.zeros(NOBS, self.n, dtype=f32, device=d)
+        self.reward = torch.zeros(self.n, dtype=f32, device=d)
+        self.term = torch.zeros(self.n, dtype=u8, device=d)
+        self.trunc = torch.zeros(self.n, dtype=u8, device=d)
+        self.info = torch.zeros(4, self.n, dtype=f32, device=d)
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and _lib._lib is not None:
+            _lib._lib.ackphys_destroy(ctx)
+            self._ctx = None
+
+    @property
+    def flags(self) -> int:
+        return CONTACTS if self.contacts else 0
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, mask: torch.Tensor | None = None, seed: int | None = None) -> torch.Tensor:
+        if seed is not None:
+            self.seed = int(seed)
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        _lib.check(_lib.lib().ackphys_reset(self._ctx, _ptr(m), self.seed, _ptr(self.state), _ptr(self.obs_soa),
+                                            self._stream()), "ackphys_reset")
+        return self.obs_soa
+
+    def step(self, actions: torch.Tensor, autoreset: bool = True, want_info: bool = True,
+             want_terminal: bool = True):
+        """actions [N,2] float32 on device. Returns SoA obs [79,N], reward, term, trunc (views of
+        the sim's buffers, overwritten by the next call)."""
+        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if actions.shape != (self.n, 2):
+            raise ValueError(f"actions must be [{self.n}, 2], got {tuple(actions.shape)}")
+        flags = self.flags | (AUTORESET if autoreset else 0)
+        _lib.check(_lib.lib().ackphys_step(
+            self._ctx, _ptr(actions), _ptr(self.state), _ptr(self.obs_soa), _ptr(self.reward), _ptr(self.term),
+            _ptr(self.trunc), _ptr(self.terminal_obs_soa) if (autoreset and want_terminal) else None,
+            _ptr(self.info) if want_info else None, flags, self.seed, self._stream()), "ackphys_step")
+        return self.obs_soa, self.reward, self.term, self.trunc
+
+    def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:
+        """[K, N, 2] i.i.d. U[-1,1) actions from Philox(seed; env, step) on device."""
+        out = torch.empty(k_steps, self.n, 2, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().ackphys_random_actions(self._ctx, _ptr(out), int(k_steps), int(seed), int(step0),
+                                                     self._stream()), "ackphys_random_actions")
+        return out
+
+    # state helpers (host-side views for tests / checkpoints)
+    def get_state(self) -> torch.Tensor:
+        return self.state.clone()
+
+    def set_state(self, state: torch.Tensor):
+        self.state.copy_(state.to(self.device, torch.float32))
