@@ -1,0 +1,185 @@
+"""Benchmark: batched Ackermann-robot env step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+A "step" is one AckermannRobotEnv.step for every env of the shard (4096 per GPU): one launch
+of ackphys_step_kernel (controller, kinematics, dynamics, contacts, Newton solve, Euler,
+lidar, obs, reward, done, auto-reset). Inputs are resident in HBM before timing: the K+W
+action batches are drawn on device from Philox (seed 0; counter = (env, step)).
+Prints ONE JSON line (rank 0).
+
+Workload (value): BASELINE.json configs[1] -- 4096 envs/GPU, random ctrl, contacts disabled.
+The contacts-enabled variant (configs[2]) is reported under "secondary".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from mujoco_playground_amd import shard  # noqa: E402
+from mujoco_playground_amd.sim import NOBS, NSTATE, BatchedAckermannSim  # noqa: E402
+
+METRIC = "env-steps/sec at 4096 envs/GPU, 1/2/4/8 MI355X; max |qpos| err vs CPU mj_step"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def algorithmic_bytes_per_env_step() -> int:
+    """Minimal HBM I/O of one env step:
+    in : state 44 words (176 B) + action 2 floats (8 B) + episode stats 4 words (16 B)
+    out: modified state words 38 (qpos 13, qvel 12, warmstart 12, step 1) = 152 B,
+         obs 79 floats (316 B), reward (4 B), term + trunc (2 B), episode stats (16 B)."""
+    return 176 + 8 + 16 + 152 + 316 + 4 + 2 + 16
+
+
+def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0):
+    sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
+                              env_offset=shard.env_offset(rank, n_env))
+    sim.reset()
+    actions = sim.random_actions(warmup + steps, seed=seed)
+    for k in range(warmup):
+        sim.step(actions[k], want_info=False)
+    stream = torch.cuda.current_stream(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    shard.barrier(world, device)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(steps):
+        sim.step(actions[warmup + k], want_info=False)
+    ev1.record(stream)
+    gathered = shard.gather_episode_stats(sim.episode, world)  # the per-rollout RCCL exchange
+    torch.cuda.synchronize(device)
+    shard.barrier(world, device)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    elapsed = shard.max_over_ranks(t1 - t0, world, device)
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    return sim, elapsed, kern_ms, shard.summarize_returns(gathered), actions
+
+
+def to_f64_state(st: torch.Tensor) -> np.ndarray:
+    s = st.detach().cpu().numpy().T.copy()
+    out = s.astype(np.float64)
+    out[:, 42] = s[:, 42].view(np.uint32)
+    out[:, 43] = s[:, 43].view(np.uint32)
+    return out
+
+
+def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s=12.0, do_timing=True):
+    """Oracle as the checker: teacher-forced max|qpos| error on a sample, and the CPU baseline
+    (oracle on the host cores, bounded sample of the same workload)."""
+    from mujoco_playground_amd import _lib
+    from oracle.oracle import FLAG_AUTORESET, FLAG_CONTACTS, Oracle
+    o = Oracle(_lib.load_blob())
+    flags = (FLAG_CONTACTS if contacts else 0) | FLAG_AUTORESET
+    # teacher-forced parity on a sample (same flags / seed as the timed run)
+    sim = BatchedAckermannSim(parity_envs, device, seed=seed, contacts=contacts)
+    sim.reset()
+    acts = sim.random_actions(parity_steps, seed=seed)
+    eq = ev = eo = 0.0
+    for k in range(parity_steps):
+        s_before = to_f64_state(sim.state)
+        sim.step(acts[k], want_info=False)
+        torch.cuda.synchronize(device)
+        s_after = to_f64_state(sim.state)
+        oobs, orew, _, _, _, _ = o.step(s_before, acts[k].cpu().numpy(), flags=flags, seed=seed)
+        eq = max(eq, float(np.abs(s_after[:, 0:13] - s_before[:, 0:13]).max()))
+        ev = max(ev, float(np.abs(s_after[:, 13:25] - s_before[:, 13:25]).max()))
+        eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs).max()))
+    parity = {"max_abs_qpos_err": eq, "max_abs_qvel_err": ev, "max_abs_obs_err": eo,
+              "sample": f"{parity_envs} envs x {parity_steps} teacher-forced steps from reset (f32 GPU vs f64 oracle)"}
+    if not do_timing:
+        return parity, None
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    n = 4096
+    st = np.zeros((n, NSTATE))
+    o.reset(st, seed=seed)
+    rng_acts = BatchedAckermannSim(n, device, seed=seed, contacts=contacts).random_actions(400, seed=seed).cpu().numpy()
+    # probe, then size the sample to ~budget_s of CPU work
+    t0 = time.perf_counter()
+    o.step(st, rng_acts[0], flags=flags, seed=seed, nthreads=threads)
+    probe = time.perf_counter() - t0
+    k = int(max(5, min(399, budget_s / max(probe, 1e-6))))
+    t0 = time.perf_counter()
+    for i in range(1, k + 1):
+        o.step(st, rng_acts[i], flags=flags, seed=seed, nthreads=threads)
+    dt = time.perf_counter() - t0
+    base = {"value": n * k / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ackphys_oracle.c (f64 restatement of mj_step + env glue), {n} envs x {k} steps "
+                      f"from reset, same Philox actions/flags, OpenMP {threads} threads, {dt:.1f} s"}
+    return parity, base
+
+
+def load_traffic(kern_name="ackphys_step_kernel"):
+    path = os.path.join(HERE, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kern_name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--contacts", type=int, default=0, help="0 = configs[1] (default), 1 = configs[2]")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    a = ap.parse_args()
+    rank, world, local = shard.init()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    contacts = bool(a.contacts)
+    sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device)
+    total_envs = a.envs * world
+    value = total_envs * a.steps / elapsed
+    secondary = None
+    if not a.no_secondary:
+        _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device)
+        secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
+                     "kernel_ms": km2}
+    parity = base = None
+    if rank == 0 and not a.no_cpu:
+        parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
+    bpe = algorithmic_bytes_per_env_step()
+    achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic()
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox random actions from "
+            "the reference reset state; random goals)",
+            "config": {"workload": f"ackermann_robot_v2.xml, {a.envs} envs/GPU, random ctrl, contacts "
+                                   f"{'enabled' if contacts else 'disabled'} (BASELINE configs[{2 if contacts else 1}])",
+                       "envs_per_gpu": a.envs, "total_envs": total_envs, "episode_len": 1000,
+                       "parallelism": f"dp{world} (independent env shards, 1 all_gather of episode stats)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ackphys_step_kernel", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_env_step": bpe,
+                         "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
+            "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,8 @@
  *  reward [N], term [N] (uint8), trunc [N] (uint8)
  *  terminal_obs [79][N] (nullable): observation before auto-reset, written for done envs
  *  info   [4][N]  (nullable): min_lidar, collision, goal_distance, bad_state
+ *  episode [4][N] (nullable, in/out): Monitor-wrapper statistics (src/rl/train.py:70):
+ *           running return, running length, sum of completed-episode returns, completed count
  */
 #ifndef ACKPHYS_H
 #define ACKPHYS_H
@@ -61,13 +63,25 @@ typedef struct ackphys_ctx ackphys_t;
 int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device, ackphys_t** out);
 int ackphys_destroy(ackphys_t* ctx);
 
+/* AckermannRobotEnv.__init__ keyword arguments (ackermann_env.py:51-60); defaults
+ * 1000 / 0.5 / 0.15 / 1.0 / 1.0 are in effect until this is called. */
+typedef struct ackphys_env_params {
+  int32_t max_episode_steps;
+  double goal_distance_threshold;
+  double collision_threshold;
+  double max_linear_velocity;
+  double max_angular_velocity;
+} ackphys_env_params;
+int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
+
 /* Global index of this context's env 0 (multi-GPU sharding: rank r passes r*n_env); it keys
  * the Philox streams for goals so a sharded run is identical to an unsharded one. */
 int ackphys_set_env_offset(ackphys_t* ctx, int64_t env_offset);
 
 /* One environment step for all N envs (replaces AckermannRobotEnv.step). */
 int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, float* reward, uint8_t* term,
-                 uint8_t* trunc, float* terminal_obs, float* info, uint32_t flags, uint64_t seed, void* stream);
+                 uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags, uint64_t seed,
+                 void* stream);
 
 /* Reset the envs whose mask byte is non-zero (mask NULL = all) (replaces
  * AckermannRobotEnv.reset): spawner pose, zero velocities, Philox(seed, env, episode) goal,

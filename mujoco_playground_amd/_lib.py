@@ -25,6 +25,13 @@ class ExtensionMissing(RuntimeError):
     pass
 
 
+class EnvParams(C.Structure):
+    """ackphys_env_params (include/ackphys.h) = AckermannRobotEnv.__init__ kwargs."""
+    _fields_ = [("max_episode_steps", C.c_int32), ("goal_distance_threshold", C.c_double),
+                ("collision_threshold", C.c_double), ("max_linear_velocity", C.c_double),
+                ("max_angular_velocity", C.c_double)]
+
+
 def build(verbose: bool = False, force: bool = False) -> str:
     """Compile csrc/ackphys_step.hip for gfx950 into csrc/build/libackphys.so (in-tree)."""
     if not force and os.path.exists(LIB_PATH):
@@ -43,7 +50,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     return LIB_PATH
 
 
-EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
+EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
 _lib = None
@@ -65,7 +72,8 @@ def lib():
     L.ackphys_create.argtypes = [C.c_char_p, sz, i32, i32, C.POINTER(P)]
     L.ackphys_destroy.argtypes = [P]
     L.ackphys_set_env_offset.argtypes = [P, i64]
-    L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, u32, u64, P]
+    L.ackphys_set_env_params.argtypes = [P, C.POINTER(EnvParams)]
+    L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, P, u32, u64, P]
     L.ackphys_reset.argtypes = [P, P, u64, P, P, P]
     L.ackphys_random_actions.argtypes = [P, P, i32, u64, u32, P]
     L.ackphys_model_fnv.restype = u64

@@ -37,9 +37,11 @@ constexpr int MAXIT = 16;        // Newton iterations cap (MuJoCo: 100; converge
 constexpr int LSIT = 12;         // line-search iterations cap
 constexpr float MINVAL = 1e-15f;
 
-// env constants (ackermann_env.py:51-60; controller.py:85-86)
-constexpr int MAX_STEPS = 1000;
-constexpr float GOAL_THRESH = 0.5f, COLL_THRESH = 0.15f;
+// env parameters: AckermannRobotEnv.__init__ kwargs (ackermann_env.py:51-60)
+struct EnvParams {
+  int max_episode_steps;
+  float goal_distance_threshold, collision_threshold, max_linear_velocity, max_angular_velocity;
+};
 
 struct Args {
   const float* action;
@@ -50,6 +52,8 @@ struct Args {
   uint8_t* trunc;
   float* tobs;
   float* info;
+  float* ep;  // [4][N] running return, running length, completed-return sum, completed episodes
+  EnvParams prm;
   int n;
   uint32_t flags;
   uint64_t seed;
@@ -82,12 +86,13 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // ------------------------------------------------------------------ controller (f64)
 // BicycleController.cmd_vel_to_controls + apply_cmd_vel, controller.py:98-140, evaluated in
 // float64 exactly like the reference (its thresholds 1e-6 / 1e-5 sit on f64 values).
-__device__ void controller(float a0f, float a1f, float ctrl[3], bool& bad) {
-  double a0 = a0f, a1 = a1f;
-  a0 = a0 < -1.0 ? -1.0 : (a0 > 1.0 ? 1.0 : a0);
-  a1 = a1 < -1.0 ? -1.0 : (a1 > 1.0 ? 1.0 : a1);
+__device__ void controller(float a0f, float a1f, float max_lin, float max_ang, float ctrl[3], bool& bad) {
+  // np.clip on the float32 action, then action * max_velocity: float32 x Python float stays
+  // float32 under NumPy 2 promotion (ackermann_env.py:190-194); controller works in float64
+  a0f = a0f < -1.0f ? -1.0f : (a0f > 1.0f ? 1.0f : a0f);
+  a1f = a1f < -1.0f ? -1.0f : (a1f > 1.0f ? 1.0f : a1f);
   const double L = 0.20, T = 0.174, rw = 0.0325, eps = 1e-5;
-  double v = a0 * 1.0, om = a1 * 1.0, delta;
+  double v = (double)(a0f * max_lin), om = (double)(a1f * max_ang), delta;
   if (fabs(om) < 1e-6) delta = 0.0;
   else {
     double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
@@ -142,7 +147,7 @@ __device__ __forceinline__ void rot_axis(float r[3], const float s[3], const flo
 struct ObsOut { float minl, dist, reward; bool term, coll; };
 
 __device__ ObsOut observe_head(const float p[3], const float q[4], const float R[9], float gx, float gy,
-                               const float ref[3], float out8[7]) {
+                               const float ref[3], float out8[7], const EnvParams& prm) {
   // odometry (odometry.py:62-103, 154-170)
   float x = p[0] - ref[0], y = p[1] - ref[1];
   float yaw = atan2f(2 * (q[0] * q[3] + q[1] * q[2]), 1 - 2 * (q[2] * q[2] + q[3] * q[3]));
@@ -153,7 +158,7 @@ __device__ ObsOut observe_head(const float p[3], const float q[4], const float R
   out8[0] = x; out8[1] = y; out8[2] = yaw; out8[3] = dx; out8[4] = dy; out8[5] = dist; out8[6] = ang;
   ObsOut o;
   o.dist = dist;
-  o.term = dist < GOAL_THRESH;
+  o.term = dist < prm.goal_distance_threshold;
   return o;
 }
 
@@ -173,9 +178,9 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
 __device__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
-                          const float ref[3], float* dst, int n) {
+                          const float ref[3], float* dst, int n, const EnvParams& prm) {
   float head[7];
-  ObsOut o = observe_head(p, q, R, gx, gy, ref, head);
+  ObsOut o = observe_head(p, q, R, gx, gy, ref, head, prm);
   // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
@@ -191,7 +196,7 @@ __device__ ObsOut observe(const float p[3], const float q[4], const float R[9], 
 #pragma unroll
   for (int k = 0; k < 7; k++) dst[(size_t)(72 + k) * n] = head[k];
   o.minl = minl;
-  o.coll = minl < COLL_THRESH;
+  o.coll = minl < prm.collision_threshold;
   float r = 0.0f;
   r -= o.dist * 0.1f;
   if (o.term) r += 100.0f;
@@ -1102,7 +1107,8 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
 }
 
 // reset env e: writes state words + observation
-__device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode) {
+__device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode,
+                          const EnvParams& prm) {
   float qpos[13], qvel[NV], warm[NV];
   reset_pose(qpos, qvel, warm);
   float gx, gy;
@@ -1125,7 +1131,7 @@ __device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed,
   for (int k = 0; k < 3; k++) state[(size_t)(ST_REF + k) * n + e] = ref[k];
   state[(size_t)ST_STEP * n + e] = __uint_as_float(0u);
   state[(size_t)ST_EPIS * n + e] = __uint_as_float(episode);
-  observe(qpos, q, R, gx, gy, ref, obs + e, n);
+  observe(qpos, q, R, gx, gy, ref, obs + e, n, prm);
 }
 
 }  // namespace ak
@@ -1157,7 +1163,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
   // controller -> ctrl (float64, reference thresholds)
   float ctrl[3];
   bool badctrl;
-  controller(a0, a1, ctrl, badctrl);
+  controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
 
   // mj_checkPos / mj_checkVel: bad state -> mj_resetData (qpos0, zero velocity/warmstart/ctrl)
   bool bad_state = false;
@@ -1193,16 +1199,28 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
 
     // observation / reward on the pre-integration pose
     const uint32_t nstep = step + 1;
-    const bool trunc = nstep >= (uint32_t)MAX_STEPS;
+    const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
     float head[7];
-    ObsOut oh = observe_head(qpos, q, R, gx, gy, ref, head);
+    ObsOut oh = observe_head(qpos, q, R, gx, gy, ref, head, A.prm);
     const bool done_pre = oh.term || trunc;
     const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
     float* dst = (autoreset && A.tobs) ? A.tobs + e : A.obs + e;
-    ObsOut o = observe(qpos, q, R, gx, gy, ref, dst, n);
+    ObsOut o = observe(qpos, q, R, gx, gy, ref, dst, n, A.prm);
     A.reward[e] = o.reward;
     A.term[e] = o.term ? 1 : 0;
     A.trunc[e] = trunc ? 1 : 0;
+    if (A.ep) {
+      // Monitor-wrapper episode bookkeeping (train.py:70): r/l of finished episodes
+      float ret = A.ep[e] + o.reward, len = A.ep[(size_t)n + e] + 1.0f;
+      if (o.term || trunc) {
+        A.ep[2 * (size_t)n + e] += ret;
+        A.ep[3 * (size_t)n + e] += 1.0f;
+        ret = 0.0f;
+        len = 0.0f;
+      }
+      A.ep[e] = ret;
+      A.ep[(size_t)n + e] = len;
+    }
     if (A.info) {
       A.info[e] = o.minl;
       A.info[(size_t)n + e] = o.coll ? 1.0f : 0.0f;
@@ -1211,7 +1229,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     }
 
     if (autoreset) {
-      reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1);
+      reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1, A.prm);
       return;
     }
     // mj_Euler: qvel += h acc (u coords -> world linear), integrate positions
@@ -1259,12 +1277,13 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
 }
 
 extern "C" __global__ void __launch_bounds__(256) ackphys_reset_kernel(const uint8_t* mask, float* state, float* obs,
-                                                                       int n, uint64_t seed, int64_t env_offset) {
+                                                                       int n, uint64_t seed, int64_t env_offset,
+                                                                       EnvParams prm) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   if (mask && !mask[e]) return;
   uint32_t episode = __float_as_uint(state[(size_t)ST_EPIS * n + e]) + 1u;
-  reset_env(state, obs, n, e, seed, env_offset + e, episode);
+  reset_env(state, obs, n, e, seed, env_offset + e, episode, prm);
 }
 
 extern "C" __global__ void __launch_bounds__(256) ackphys_actions_kernel(float* actions, int n, int k_steps,
@@ -1289,6 +1308,7 @@ struct ackphys_ctx {
   int n_env;
   int device;
   int64_t env_offset;
+  ak::EnvParams prm;
 };
 
 static thread_local char g_err[512];
@@ -1332,12 +1352,21 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
   c->n_env = n_env;
   c->device = device;
   c->env_offset = 0;
+  c->prm = ak::EnvParams{1000, 0.5f, 0.15f, 1.0f, 1.0f};  // AckermannRobotEnv defaults
   *out = c;
   return ACKPHYS_OK;
 }
 
 int ackphys_destroy(ackphys_t* ctx) {
   delete ctx;
+  return ACKPHYS_OK;
+}
+
+int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* p) {
+  if (!ctx || !p) return fail(ACKPHYS_EINVAL, "ackphys_set_env_params: NULL argument");
+  if (p->max_episode_steps <= 0) return fail(ACKPHYS_EINVAL, "max_episode_steps must be positive");
+  ctx->prm = ak::EnvParams{p->max_episode_steps, (float)p->goal_distance_threshold, (float)p->collision_threshold,
+                           (float)p->max_linear_velocity, (float)p->max_angular_velocity};
   return ACKPHYS_OK;
 }
 
@@ -1348,12 +1377,14 @@ int ackphys_set_env_offset(ackphys_t* ctx, int64_t off) {
 }
 
 int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, float* reward, uint8_t* term,
-                 uint8_t* trunc, float* terminal_obs, float* info, uint32_t flags, uint64_t seed, void* stream) {
+                 uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags, uint64_t seed,
+                 void* stream) {
   if (!ctx || !action || !state || !obs || !reward || !term || !trunc)
     return fail(ACKPHYS_EINVAL, "ackphys_step: NULL argument");
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hipfail(e, "hipSetDevice");
-  ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, ctx->n_env, flags, seed, ctx->env_offset};
+  ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
+             ctx->env_offset};
   int blocks = (ctx->n_env + 63) / 64;
   hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
   e = hipGetLastError();
@@ -1367,7 +1398,7 @@ int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* sta
   if (e != hipSuccess) return hipfail(e, "hipSetDevice");
   int blocks = (ctx->n_env + 255) / 256;
   hipLaunchKernelGGL(ackphys_reset_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
-                     ctx->n_env, seed, ctx->env_offset);
+                     ctx->n_env, seed, ctx->env_offset, ctx->prm);
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_reset_kernel launch");
   return ACKPHYS_OK;

@@ -1,0 +1,75 @@
+"""AckermannRobotEnv: the reference's single-env Gym surface on the batched HIP simulator.
+
+Mirrors src/rl/envs/ackermann_env.py:33-325 (same constructor kwargs, observation/action
+spaces, reset()/step() return tuples and info keys) with N=1 on the GPU. Used for the
+reference's 1-env call paths (train.py random baseline, evaluate_agent); batched training uses
+AckermannVecEnv. There is no CPU fallback: a missing HIP build raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ...sim import BatchedAckermannSim
+from .. import spaces
+
+
+class AckermannRobotEnv:
+    metadata = {"render_modes": ["human", "rgb_array"], "render_fps": 50}
+
+    def __init__(self, map_spawner=None, max_episode_steps=1000, goal_distance_threshold=0.5,
+                 collision_threshold=0.15, max_linear_velocity=1.0, max_angular_velocity=1.0, render_mode=None,
+                 device="cuda:0", contacts: bool = True):
+        if render_mode == "human":
+            raise NotImplementedError("render_mode='human' (MuJoCo viewer) is out of scope (SURVEY.md §2)")
+        self.max_episode_steps = max_episode_steps
+        self.goal_distance_threshold = goal_distance_threshold
+        self.collision_threshold = collision_threshold
+        self.max_linear_velocity = max_linear_velocity
+        self.max_angular_velocity = max_angular_velocity
+        self.render_mode = render_mode
+        self.observation_space = spaces.observation_space()
+        self.action_space = spaces.action_space()
+        self._sim = BatchedAckermannSim(1, device, seed=0, contacts=contacts, max_episode_steps=max_episode_steps,
+                                        goal_distance_threshold=goal_distance_threshold,
+                                        collision_threshold=collision_threshold,
+                                        max_linear_velocity=max_linear_velocity,
+                                        max_angular_velocity=max_angular_velocity)
+        self._rng = np.random.default_rng()
+        self.step_count = 0
+        self.goal_position = None
+        self.robot_start_position = None
+
+    def reset(self, seed=None, options=None):
+        if seed is not None:
+            self._rng = np.random.default_rng(seed)
+        # goals come from Philox(seed, env, episode) on the device; draw the seed host-side
+        self._sim.reset(seed=int(self._rng.integers(0, 2**63 - 1)))
+        self.step_count = 0
+        st = self._sim.state[:, 0].cpu().numpy()
+        self.goal_position = st[37:39].astype(np.float64)
+        self.robot_start_position = np.zeros(2)
+        obs = self._sim.obs_soa[:, 0].cpu().numpy().astype(np.float32)
+        info = {"map_name": "simple_floor", "goal_position": self.goal_position.tolist(),
+                "start_position": self.robot_start_position.tolist()}
+        return obs, info
+
+    def step(self, action):
+        a = np.clip(np.asarray(action, dtype=np.float32).reshape(2), -1.0, 1.0)
+        act = torch.as_tensor(a, device=self._sim.device).reshape(1, 2)
+        obs, rew, term, trunc = self._sim.step(act, autoreset=False)
+        self.step_count += 1
+        o = obs[:, 0].cpu().numpy().astype(np.float32)
+        info_t = self._sim.info[:, 0].cpu().numpy()
+        terminated = bool(term[0].item())
+        truncated = bool(trunc[0].item())
+        info = {"goal_distance": float(info_t[2]), "collision": bool(info_t[1] > 0), "min_lidar": float(info_t[0]),
+                "step": self.step_count, "linear_velocity": float(a[0] * np.float32(self.max_linear_velocity)),
+                "angular_velocity": float(a[1] * np.float32(self.max_angular_velocity))}
+        return o, float(rew[0].item()), terminated, truncated, info
+
+    def render(self):
+        return None
+
+    def close(self):
+        pass

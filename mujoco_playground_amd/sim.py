@@ -25,7 +25,9 @@ def _ptr(t):
 
 class BatchedAckermannSim:
     def __init__(self, num_envs: int, device="cuda:0", seed: int = 0, contacts: bool = True,
-                 env_offset: int = 0, model_blob: bytes | None = None):
+                 env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
+                 goal_distance_threshold: float = 0.5, collision_threshold: float = 0.15,
+                 max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
@@ -38,6 +40,9 @@ class BatchedAckermannSim:
         _lib.check(L.ackphys_create(blob, len(blob), self.n, self.device.index or 0, C.byref(ctx)), "ackphys_create")
         self._ctx = ctx
         _lib.check(L.ackphys_set_env_offset(ctx, int(env_offset)), "ackphys_set_env_offset")
+        self.params = _lib.EnvParams(int(max_episode_steps), float(goal_distance_threshold), float(collision_threshold),
+                                     float(max_linear_velocity), float(max_angular_velocity))
+        _lib.check(L.ackphys_set_env_params(ctx, C.byref(self.params)), "ackphys_set_env_params")
         f32, u8 = torch.float32, torch.uint8
         d = self.device
         self.state = torch.zeros(NSTATE, self.n, dtype=f32, device=d)
@@ -47,6 +52,7 @@ class BatchedAckermannSim:
         self.term = torch.zeros(self.n, dtype=u8, device=d)
         self.trunc = torch.zeros(self.n, dtype=u8, device=d)
         self.info = torch.zeros(4, self.n, dtype=f32, device=d)
+        self.episode = torch.zeros(4, self.n, dtype=f32, device=d)
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
@@ -72,7 +78,7 @@ class BatchedAckermannSim:
         return self.obs_soa
 
     def step(self, actions: torch.Tensor, autoreset: bool = True, want_info: bool = True,
-             want_terminal: bool = True):
+             want_terminal: bool = True, track_episodes: bool = True):
         """actions [N,2] float32 on device. Returns SoA obs [79,N], reward, term, trunc (views of
         the sim's buffers, overwritten by the next call)."""
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
@@ -83,7 +89,8 @@ class BatchedAckermannSim:
         _lib.check(_lib.lib().ackphys_step(
             self._ctx, _ptr(actions), _ptr(self.state), _ptr(self.obs_soa), _ptr(self.reward), _ptr(self.term),
             _ptr(self.trunc), _ptr(self.terminal_obs_soa) if (autoreset and want_terminal) else None,
-            _ptr(self.info) if want_info else None, flags, self.seed, self._stream()), "ackphys_step")
+            _ptr(self.info) if want_info else None, _ptr(self.episode) if track_episodes else None, flags,
+            self.seed, self._stream()), "ackphys_step")
         return self.obs_soa, self.reward, self.term, self.trunc
 
     def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:

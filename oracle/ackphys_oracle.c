@@ -53,12 +53,7 @@
 #define FLAG_CONTACTS 1u
 #define FLAG_AUTORESET 2u
 
-/* env constants: ackermann_env.py:51-60 defaults, controller.py:85-86 */
-#define ENV_MAX_STEPS 1000
-#define ENV_GOAL_THRESH 0.5
-#define ENV_COLL_THRESH 0.15
-#define ENV_MAX_LIN 1.0
-#define ENV_MAX_ANG 1.0
+/* controller constants: controller.py:85-86 */
 #define CTL_WHEEL_R 0.0325
 #define CTL_WHEELBASE 0.20
 #define CTL_TRACK 0.174
@@ -72,6 +67,9 @@ typedef struct {
   double tolerance;
   int maxiter;
   int env_offset;
+  /* AckermannRobotEnv.__init__ kwargs (ackermann_env.py:51-60) */
+  int max_steps;
+  double goal_thresh, coll_thresh, max_lin, max_ang;
   /* resolved ids (reference looks these up by name) */
   int chassis_body, act_steer, act_rl, act_rr;
   int lidar_adr[72];
@@ -269,6 +267,7 @@ int or_create(const void* blob, size_t nbytes, or_ctx** out) {
   c->tolerance = 1e-12; /* tighter than MuJoCo's 1e-8: the oracle targets the exact optimum */
   c->maxiter = c->m->iterations;
   c->chassis_body = 1;
+  c->max_steps = 1000; c->goal_thresh = 0.5; c->coll_thresh = 0.15; c->max_lin = 1.0; c->max_ang = 1.0;
   /* BicycleController actuator lookup by name (controller.py:94-96): steering servo on the
      first limited hinge, rear drives on the first two hinges -- resolved by trnid order. */
   c->act_steer = 0; c->act_rl = 1; c->act_rr = 2;
@@ -296,6 +295,9 @@ void or_destroy(or_ctx* c) {
 
 void or_set_solver(or_ctx* c, double tolerance, int maxiter) { c->tolerance = tolerance; c->maxiter = maxiter; }
 void or_set_env_offset(or_ctx* c, int off) { c->env_offset = off; }
+void or_set_env_params(or_ctx* c, int max_steps, double goal, double coll, double max_lin, double max_ang) {
+  c->max_steps = max_steps; c->goal_thresh = goal; c->coll_thresh = coll; c->max_lin = max_lin; c->max_ang = max_ang;
+}
 
 /* ------------------------------------------------------------------ mj_kinematics */
 
@@ -1302,11 +1304,13 @@ static void mj_step(const or_ctx* c, or_data* d, uint32_t flags) {
 /* ------------------------------------------------------------------ env glue */
 
 /* BicycleController.cmd_vel_to_controls + apply_cmd_vel (controller.py:98-140); ctrl[3] */
-void or_controller(const float action[2], double ctrl[3]) {
-  double a0 = action[0], a1 = action[1];
-  a0 = a0 < -1 ? -1 : (a0 > 1 ? 1 : a0);
-  a1 = a1 < -1 ? -1 : (a1 > 1 ? 1 : a1);
-  double v = a0 * ENV_MAX_LIN, omega = a1 * ENV_MAX_ANG, eps = 1e-5, delta;
+void or_controller2(const float action[2], double max_lin, double max_ang, double ctrl[3]) {
+  /* np.clip of the float32 action; action[i] * python float stays float32 (NumPy 2 promotion) */
+  float a0 = action[0], a1 = action[1];
+  a0 = a0 < -1.0f ? -1.0f : (a0 > 1.0f ? 1.0f : a0);
+  a1 = a1 < -1.0f ? -1.0f : (a1 > 1.0f ? 1.0f : a1);
+  volatile float lx = a0 * (float)max_lin, az = a1 * (float)max_ang;
+  double v = (double)lx, omega = (double)az, eps = 1e-5, delta;
   if (fabs(omega) < 1e-6) delta = 0.0;
   else {
     double den = fabs(v) > eps ? v : ((omega > 0) - (omega < 0)) * eps;
@@ -1330,6 +1334,8 @@ void or_controller(const float action[2], double ctrl[3]) {
   double c2 = isnan(wr) ? wr : (wr < -50 ? -50 : (wr > 50 ? 50 : wr));
   ctrl[0] = c0; ctrl[1] = c1; ctrl[2] = c2;
 }
+
+void or_controller(const float action[2], double ctrl[3]) { or_controller2(action, 1.0, 1.0, ctrl); }
 
 /* odometry yaw (odometry.py:154-170) */
 static double quat_yaw(const double q[4]) {
@@ -1356,8 +1362,8 @@ static void observe(const or_ctx* c, const or_data* d, const double goal[2], con
     double v = d->sensordata[c->lidar_adr[i]];
     if (v < minl) minl = v;
   }
-  int coll = minl < ENV_COLL_THRESH;
-  int t = dist < ENV_GOAL_THRESH;
+  int coll = minl < c->coll_thresh;
+  int t = dist < c->goal_thresh;
   double r = 0.0;
   r -= dist * 0.1;
   if (t) r += 100.0;
@@ -1414,7 +1420,7 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
                      double* terminal_obs, double info[4]) {
   load_state(c, d, st);
   double ctrl[3];
-  or_controller(action, ctrl);
+  or_controller2(action, c->max_lin, c->max_ang, ctrl);
   d->bad_ctrl = 0;
   for (int k = 0; k < 3; k++)
     if (is_bad(ctrl[k])) d->bad_ctrl = 1;
@@ -1428,7 +1434,7 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
   observe(c, d, st + ST_GOAL, st + ST_REF, obs, reward, &t, inf3);
   store_state(c, d, st);
   st[ST_STEP] += 1;
-  int tr = st[ST_STEP] >= ENV_MAX_STEPS;
+  int tr = st[ST_STEP] >= c->max_steps;
   *term = (uint8_t)t;
   *trunc = (uint8_t)tr;
   if (info) { info[0] = inf3[0]; info[1] = inf3[1]; info[2] = inf3[2]; info[3] = d->bad_state; }
@@ -1436,6 +1442,19 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
     if (terminal_obs) memcpy(terminal_obs, obs, sizeof(double) * NOBS);
     env_reset(c, d, st, env, seed, obs);
   }
+}
+
+/* golden-vector entry: _get_observation/_calculate_reward from raw mjData fields */
+int or_observe_raw(const or_ctx* c, const double xpos[3], const double xquat[4], const double* sensordata,
+                   const double goal[2], const double ref[3], double obs[NOBS], double* reward, int* term,
+                   double info[3]) {
+  or_data* d = (or_data*)calloc(1, sizeof(or_data));
+  memcpy(d->xpos[c->chassis_body], xpos, sizeof(double) * 3);
+  memcpy(d->xquat[c->chassis_body], xquat, sizeof(double) * 4);
+  memcpy(d->sensordata, sensordata, sizeof(double) * c->m->nsensordata);
+  observe(c, d, goal, ref, obs, reward, term, info);
+  free(d);
+  return 0;
 }
 
 /* ------------------------------------------------------------------ exported batch API */

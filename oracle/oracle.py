@@ -51,8 +51,11 @@ def lib():
         L.or_step_diag.argtypes = [P, P, P, u32, P]
         L.or_step_diag.restype = i32
         L.or_controller.argtypes = [P, P]
+        L.or_controller2.argtypes = [P, C.c_double, C.c_double, P]
+        L.or_set_env_params.argtypes = [P, i32, C.c_double, C.c_double, C.c_double, C.c_double]
         L.or_philox.argtypes = [P, P, P]
         L.or_model_struct_size.restype = i32
+        L.or_observe_raw.argtypes = [P, P, P, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -76,6 +79,11 @@ class Oracle:
 
     def set_solver(self, tolerance: float = 1e-12, maxiter: int = 100):
         lib().or_set_solver(self._ctx, tolerance, maxiter)
+
+    def set_env_params(self, max_episode_steps=1000, goal_distance_threshold=0.5, collision_threshold=0.15,
+                       max_linear_velocity=1.0, max_angular_velocity=1.0):
+        lib().or_set_env_params(self._ctx, max_episode_steps, goal_distance_threshold, collision_threshold,
+                                max_linear_velocity, max_angular_velocity)
 
     def set_env_offset(self, off: int):
         lib().or_set_env_offset(self._ctx, off)
@@ -102,6 +110,14 @@ class Oracle:
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         lib().or_reset_batch(self._ctx, n, _p(m), seed, _p(states), _p(obs))
         return obs
+
+    def observe_raw(self, xpos, xquat, sensordata, goal, ref):
+        """(obs[79], reward, terminated, (min_lidar, collision, goal_distance)) from raw mjData."""
+        f = lambda x: np.ascontiguousarray(x, dtype=np.float64)
+        obs, rew, term, info = np.zeros(NOBS), np.zeros(1), C.c_int(0), np.zeros(3)
+        lib().or_observe_raw(self._ctx, _p(f(xpos)), _p(f(xquat)), _p(f(sensordata)), _p(f(goal)), _p(f(ref)),
+                             _p(obs), _p(rew), C.byref(term), _p(info))
+        return obs, float(rew[0]), bool(term.value), info
 
     def diag(self, state: np.ndarray, ctrl, flags: int = FLAG_CONTACTS, nv: int = 12, nq: int = 13,
              nsensordata: int = 77) -> dict:
@@ -140,10 +156,10 @@ class Oracle:
         return r
 
 
-def controller(action) -> np.ndarray:
+def controller(action, max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0) -> np.ndarray:
     a = np.ascontiguousarray(action, dtype=np.float32).reshape(2)
     out = np.zeros(3)
-    lib().or_controller(_p(a), _p(out))
+    lib().or_controller2(_p(a), max_linear_velocity, max_angular_velocity, _p(out))
     return out
 
 

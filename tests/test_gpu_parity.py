@@ -1,0 +1,233 @@
+"""GPU (MI355X) parity of libackphys.so against the f64 CPU oracle.
+
+Tolerances (stated, f32 kernel vs f64 oracle, teacher-forced = both start every step from the
+same GPU state): |dqpos| <= 1e-5, |dqvel| <= 1e-3, obs <= 1e-4 abs (+1e-5 rel), reward <= 1e-4.
+Measured on MI355X: |dqpos| ~2e-7, |dqvel| ~3e-5. Discrete outputs
+(terminated/truncated, reset goals' Philox draws, action streams) must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import f64_state
+
+pytestmark = pytest.mark.gpu
+
+TOL_QPOS, TOL_QVEL, TOL_OBS, TOL_REW = 1e-5, 1e-3, 1e-4, 1e-4
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def make_sim(n, **kw):
+    from mujoco_playground_amd.sim import BatchedAckermannSim
+    return BatchedAckermannSim(n, DEV, **kw)
+
+
+def fresh_oracle(blob, **params):
+    from oracle.oracle import Oracle
+    o = Oracle(blob)
+    if params:
+        o.set_env_params(**params)
+    return o
+
+
+def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
+    worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0)
+    for k in range(steps):
+        before = f64_state(sim.state)
+        sim.step(acts[k], autoreset=bool(flags & 2))
+        torch.cuda.synchronize()
+        after = f64_state(sim.state)
+        ref = before.copy()
+        oobs, orew, oterm, otr, tobs, _ = o.step(ref, acts[k].cpu().numpy(), flags=flags, seed=seed, terminal=True)
+        dq = np.abs(after[:, :13] - ref[:, :13]).max()
+        dv = np.abs(after[:, 13:25] - ref[:, 13:25]).max()
+        worst["qpos"], worst["qvel"] = max(worst["qpos"], dq), max(worst["qvel"], dv)
+        assert dq <= TOL_QPOS, f"step {k}: |dqpos| {dq}"
+        assert dv <= TOL_QVEL, f"step {k}: |dqvel| {dv}"
+        np.testing.assert_array_equal(sim.term.cpu().numpy().astype(bool), oterm)
+        np.testing.assert_array_equal(sim.trunc.cpu().numpy().astype(bool), otr)
+        np.testing.assert_array_equal(after[:, 42:44], ref[:, 42:44])
+        if check_obs:
+            gobs = sim.obs_soa.cpu().numpy().T
+            do = np.abs(gobs - oobs) / (1.0 + 0.1 * np.abs(oobs))
+            worst["obs"] = max(worst["obs"], do.max())
+            assert do.max() <= TOL_OBS, f"step {k}: obs {do.max()}"
+            dr = np.abs(sim.reward.cpu().numpy() - orew).max()
+            worst["rew"] = max(worst["rew"], dr)
+            assert dr <= TOL_REW
+    return worst
+
+
+def test_reset_matches_oracle(blob):
+    n = 300  # not a multiple of 64: partial last block
+    sim = make_sim(n, seed=7)
+    sim.reset()
+    torch.cuda.synchronize()
+    o = fresh_oracle(blob)
+    st = np.zeros((n, 44))
+    oobs = o.reset(st, seed=7)
+    g = f64_state(sim.state)
+    np.testing.assert_allclose(g[:, :37], st[:, :37], atol=1e-7)
+    np.testing.assert_allclose(g[:, 37:39], st[:, 37:39], atol=1e-5)   # goals: f32 trig of the same Philox draws
+    np.testing.assert_array_equal(g[:, 42:44], st[:, 42:44])
+    np.testing.assert_allclose(sim.obs_soa.cpu().numpy().T, oobs, atol=1e-5)
+
+
+@pytest.mark.parametrize("contacts", [True, False])
+def test_teacher_forced_step(blob, contacts):
+    n, steps, seed = 256, 150, 11
+    sim = make_sim(n, seed=seed, contacts=contacts)
+    sim.reset()
+    acts = sim.random_actions(steps, seed=seed)
+    o = fresh_oracle(blob)
+    flags = (1 if contacts else 0) | 2
+    w = teacher_forced(sim, o, acts, steps, flags, seed)
+    print("worst", contacts, w)
+
+
+def test_autoreset_truncation_terminal_obs(blob):
+    n, seed = 64, 3
+    sim = make_sim(n, seed=seed, max_episode_steps=25)
+    sim.reset()
+    acts = sim.random_actions(60, seed=seed)
+    o = fresh_oracle(blob, max_episode_steps=25)
+    st = f64_state(sim.state)
+    for k in range(60):
+        sim.step(acts[k])
+        torch.cuda.synchronize()
+        oobs, orew, oterm, otr, tobs, _ = o.step(st, acts[k].cpu().numpy(), flags=3, seed=seed, terminal=True)
+        g = f64_state(sim.state)
+        done = oterm | otr
+        assert np.array_equal(sim.trunc.cpu().numpy().astype(bool), otr)
+        if k == 24:
+            assert otr.all()
+        if done.any():
+            np.testing.assert_allclose(sim.terminal_obs_soa.cpu().numpy().T[done], tobs[done], atol=1e-4)
+            np.testing.assert_allclose(sim.obs_soa.cpu().numpy().T[done], oobs[done], atol=1e-4)
+            assert np.all(g[done, 42] == 0) and np.all(g[done, 43] == st[done, 43])
+        np.testing.assert_allclose(g[:, :25], st[:, :25], atol=5e-4)
+        st = g  # continue from the GPU state (teacher forcing)
+    ep = sim.episode.cpu().numpy()
+    assert np.all(ep[3] == 2)  # two completed episodes of 25 steps in 60
+
+
+def test_termination_bonus(blob):
+    n, seed = 64, 5
+    sim = make_sim(n, seed=seed, goal_distance_threshold=100.0)
+    sim.reset()
+    acts = sim.random_actions(2, seed=seed)
+    o = fresh_oracle(blob, goal_distance_threshold=100.0)
+    teacher_forced(sim, o, acts, 2, 3, seed)
+    assert sim.term.cpu().numpy().all()
+
+
+def test_env_params_make_env_defaults(blob):
+    """make_ackermann_env defaults (max_linear_velocity=0.5, goal threshold 0.3)."""
+    n, seed = 128, 9
+    kw = dict(max_linear_velocity=0.5, goal_distance_threshold=0.3)
+    sim = make_sim(n, seed=seed, **kw)
+    sim.reset()
+    acts = sim.random_actions(40, seed=seed)
+    teacher_forced(sim, o := fresh_oracle(blob, **kw), acts, 40, 3, seed)
+
+
+def test_random_actions_are_philox_exact():
+    from oracle.oracle import philox
+    sim = make_sim(96, seed=0, env_offset=1000)
+    a = sim.random_actions(3, seed=0x1234567890AB, step0=7).cpu().numpy()
+    for k in range(3):
+        for e in [0, 17, 95]:
+            x = philox([1000 + e, 7 + k, 1, 0], [0x567890AB, 0x1234])
+            u = ((x[:2] >> 8).astype(np.float64) / 16777216.0).astype(np.float32)
+            np.testing.assert_array_equal(a[k, e], (2 * u - 1).astype(np.float32))
+
+
+def test_bad_ctrl_nan_path(blob):
+    """action -> R = inf -> 0*inf = NaN wheel speeds in the reference controller; ctrl zeroed."""
+    n, seed = 64, 2
+    sim = make_sim(n, seed=seed)
+    sim.reset()
+    a = torch.tensor([[0.5, 6e-6]] * n, device=DEV)
+    acts = torch.stack([a] * 5)
+    teacher_forced(sim, fresh_oracle(blob), acts, 5, 3, seed)
+
+
+def test_bad_state_resets(blob):
+    n, seed = 64, 4
+    sim = make_sim(n, seed=seed)
+    sim.reset()
+    st = sim.state.clone()
+    st[13, :8] = float("nan")          # bad qvel
+    st[0, 8:16] = 3e10                  # bad qpos
+    sim.set_state(st)
+    acts = sim.random_actions(3, seed=seed)
+    teacher_forced(sim, fresh_oracle(blob), acts, 3, 3, seed)
+    assert torch.isfinite(sim.state).all()
+
+
+def test_sharding_is_exact():
+    """Two half-size shards with env offsets reproduce the unsharded run bit for bit."""
+    n, steps, seed = 128, 60, 21
+    full = make_sim(n, seed=seed, max_episode_steps=20)
+    a = make_sim(n // 2, seed=seed, env_offset=0, max_episode_steps=20)
+    b = make_sim(n // 2, seed=seed, env_offset=n // 2, max_episode_steps=20)
+    for s in (full, a, b):
+        s.reset()
+    acts_full = full.random_actions(steps, seed=seed)
+    acts_a, acts_b = a.random_actions(steps, seed=seed), b.random_actions(steps, seed=seed)
+    assert torch.equal(acts_full[:, : n // 2], acts_a) and torch.equal(acts_full[:, n // 2:], acts_b)
+    for k in range(steps):
+        full.step(acts_full[k])
+        a.step(acts_a[k])
+        b.step(acts_b[k])
+    torch.cuda.synchronize()
+    assert torch.equal(full.state, torch.cat([a.state, b.state], dim=1))
+    assert torch.equal(full.obs_soa, torch.cat([a.obs_soa, b.obs_soa], dim=1))
+
+
+def test_full_size_properties():
+    """BASELINE size (4096 envs) through truncation: size-independent invariants."""
+    n = 4096
+    sim = make_sim(n, seed=1, contacts=True)
+    sim.reset()
+    acts = sim.random_actions(1010, seed=1)
+    done_count = torch.zeros(n, device=DEV)
+    for k in range(1010):
+        _, rew, term, trunc = sim.step(acts[k], want_info=False)
+        done_count += (term | trunc).float()
+    torch.cuda.synchronize()
+    st = sim.state
+    assert torch.isfinite(st[:37]).all()
+    qn = torch.linalg.norm(st[3:7], dim=0)
+    assert (qn - 1).abs().max().item() < 1e-5
+    steps = st[42].view(torch.int32)
+    assert (steps >= 0).all() and (steps < 1000).all()
+    assert torch.equal(sim.episode[3], done_count)
+    assert (done_count >= 1).all()       # everybody truncated at least once
+    assert torch.isfinite(sim.obs_soa).all()
+
+
+def test_vec_env_and_gym_api():
+    from mujoco_playground_amd.rl import AckermannRobotEnv, make_ackermann_env
+    venv = make_ackermann_env(env_type="vec", num_envs=64, max_episode_steps=5, device=DEV)
+    obs = venv.reset()
+    assert obs.shape == (64, 79)
+    for k in range(5):
+        obs, rew, done, infos = venv.step(torch.zeros(64, 2, device=DEV))
+    assert done.all() and len(infos) == 64
+    assert infos[0]["terminal_observation"].shape == (79,) and infos[0]["TimeLimit.truncated"]
+    assert infos[0]["episode"]["l"] == 5
+    env = AckermannRobotEnv(device=DEV)
+    o, info = env.reset(seed=0)
+    assert o.shape == (79,) and o.dtype == np.float32 and set(info) == {"map_name", "goal_position",
+                                                                         "start_position"}
+    o2, r, te, tr, info = env.step(env.action_space.sample())
+    assert np.array_equal(o2, o)  # obs lag: first step returns the reset pose's observation
+    assert isinstance(r, float) and isinstance(te, bool) and isinstance(tr, bool)
+    assert set(info) >= {"goal_distance", "collision", "min_lidar", "step", "linear_velocity", "angular_velocity"}
