@@ -22,6 +22,23 @@
 
 #include "ackphys_model_gen.h"
 
+// Diagnostic build only (-DAK_STAMPS): per-wave s_memtime phase stamps, never in the product.
+#ifdef AK_STAMPS
+__device__ unsigned long long* g_stamps;
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long _t;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if ((threadIdx.x & 63) == 0) g_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;       \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 namespace ak {
 using namespace apg;
 
@@ -33,7 +50,7 @@ constexpr uint32_t F_CONTACTS = 1u, F_AUTORESET = 2u;
 constexpr int NSLOT = 24;        // 4 wheels x 4 + 2 meshes x 4 contact slots
 constexpr int NF = 13;           // Pb[3], D, jar[4], jp[4], active
 constexpr int NSCAL = 11;        // eq(1) + frictionloss(6) + limits(4)
-constexpr int MAXIT = 16;        // Newton iterations cap (MuJoCo: 100; converges in 1-4 here)
+constexpr int MAXIT = 12;        // Newton iterations cap (MuJoCo: 100; converges in 1-4 here)
 constexpr int LSIT = 12;         // line-search iterations cap
 constexpr float MINVAL = 1e-15f;
 
@@ -184,7 +201,7 @@ __device__ ObsOut observe(const float p[3], const float q[4], const float R[9], 
   // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
-#pragma unroll 2
+#pragma unroll 8
   for (int i = 10; i < 72; i++) {
     float v = ray_floor(p, R, i);
     dst[(size_t)i * n] = v;
@@ -229,6 +246,7 @@ __device__ __forceinline__ void ref_kb(float& K, float& B) {
 }
 
 // ------------------------------------------------------------------ 12x12 Cholesky
+// L L^T in the lower triangle; the diagonal holds 1/L_jj (solves multiply, never divide)
 __device__ __forceinline__ bool chol12(float A[NV][NV]) {
   bool ok = true;
 #pragma unroll
@@ -237,9 +255,8 @@ __device__ __forceinline__ bool chol12(float A[NV][NV]) {
 #pragma unroll
     for (int k = 0; k < j; k++) s -= A[j][k] * A[j][k];
     ok = ok && (s > 0.0f);
-    s = sqrtf(fmaxf(s, 1e-30f));
-    A[j][j] = s;
-    float inv = 1.0f / s;
+    float inv = __frsqrt_rn(fmaxf(s, 1e-30f));
+    A[j][j] = inv;
 #pragma unroll
     for (int i = j + 1; i < NV; i++) {
       float t = A[i][j];
@@ -256,14 +273,14 @@ __device__ __forceinline__ void chol12_solve(const float L[NV][NV], float x[NV])
     float s = x[i];
 #pragma unroll
     for (int k = 0; k < i; k++) s -= L[i][k] * x[k];
-    x[i] = s / L[i][i];
+    x[i] = s * L[i][i];
   }
 #pragma unroll
   for (int i = NV - 1; i >= 0; i--) {
     float s = x[i];
 #pragma unroll
     for (int k = i + 1; k < NV; k++) s -= L[k][i] * x[k];
-    x[i] = s / L[i][i];
+    x[i] = s * L[i][i];
   }
 }
 __device__ __forceinline__ void symv12(const float M[NV][NV], const float x[NV], float y[NV]) {
@@ -382,9 +399,16 @@ __device__ void bias(const float u[NV], const float R[9], const float sa[2][3], 
 
 // ------------------------------------------------------------------ contact slots in LDS
 struct Slots {
-  float* base;  // [NSLOT][NF][64] for this block; lane offset applied
+  float* base;     // [NSLOT][NF][64] for this block; lane offset applied
+  uint32_t lmask;  // this lane's active contact slots
+  uint32_t wmask;  // OR over the wave (uniform): loops visit only these slots
   __device__ __forceinline__ float& at(int s, int f) const { return base[(s * NF + f) * 64]; }
+  __device__ __forceinline__ bool on(int s) const { return (lmask >> s) & 1u; }
 };
+// iterate the wave-uniform set bits of m (slot indices), skipping lanes where the slot is off
+#define FOR_SLOTS(S, m, s)                  \
+  for (uint32_t _m = (m); _m; _m &= _m - 1) \
+    if (const int s = __builtin_ctz(_m); !(S).on(s)) { } else
 
 // chain geometry: contact point P (chassis frame) -> jacobian rows G[dir][8] for the 3 frame
 // directions; columns 0..5 = v_b, w_b; col 6/7 = chain hinge dofs (see dof6/dof7).
@@ -492,10 +516,7 @@ __device__ __forceinline__ void slot_loop_hess(const Slots& S, const float dirs[
                                                float H[NV][NV], float grad[NV]) {
   constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
   const float mu = chain_mu<CH>();
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) {
-    const int s = s0 + k;
-    if (S.at(s, 12) == 0.0f) continue;
+  FOR_SLOTS(S, S.wmask & (15u << s0), s) {
     float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
     float D = S.at(s, 3);
     float G[3][8];
@@ -518,10 +539,7 @@ __device__ __forceinline__ void slot_loop_jp(const Slots& S, const float dirs[3]
                                              const float p[NV]) {
   constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
   const float mu = chain_mu<CH>();
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) {
-    const int s = s0 + k;
-    if (S.at(s, 12) == 0.0f) continue;
+  FOR_SLOTS(S, S.wmask & (15u << s0), s) {
     float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
     float G[3][8];
     jac_rows<CH>(P, dirs, sa, G);
@@ -539,10 +557,7 @@ __device__ __forceinline__ void slot_loop_init(const Slots& S, const float dirs[
                                                const float a[NV], const float u[NV], float K, float B) {
   constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
   const float mu = chain_mu<CH>();
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) {
-    const int s = s0 + k;
-    if (S.at(s, 12) == 0.0f) continue;
+  FOR_SLOTS(S, S.wmask & (15u << s0), s) {
     float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
     float dist = S.at(s, 3);  // holds dist until replaced by D
     float G[3][8];
@@ -568,10 +583,7 @@ __device__ __forceinline__ void slot_loop_force(const Slots& S, const float dirs
                                                 float fc[NV]) {
   constexpr int s0 = CH < 4 ? CH * 4 : 16 + (CH - 4) * 4;
   const float mu = chain_mu<CH>();
-#pragma unroll 1
-  for (int k = 0; k < 4; k++) {
-    const int s = s0 + k;
-    if (S.at(s, 12) == 0.0f) continue;
+  FOR_SLOTS(S, S.wmask & (15u << s0), s) {
     float P[3] = {S.at(s, 0), S.at(s, 1), S.at(s, 2)};
     float D = S.at(s, 3);
     float G[3][8];
@@ -588,14 +600,10 @@ __device__ __forceinline__ void slot_loop_force(const Slots& S, const float dirs
   }
 }
 
-__device__ __forceinline__ void slot_deactivate_all(const Slots& S) {
-#pragma unroll
-  for (int s = 0; s < NSLOT; s++) S.at(s, 12) = 0.0f;
-}
 
 // plane-cylinder for wheel W: writes up to 4 slots (mjc_PlaneCylinder restatement)
 template <int W>
-__device__ __forceinline__ int wheel_contacts(const Slots& S, const float p[3], const float R[9], const float cyl_b[3]) {
+__device__ __forceinline__ uint32_t wheel_contacts(const Slots& S, const float p[3], const float R[9], const float cyl_b[3]) {
   constexpr int s0 = W * 4;
   float c[3], axis[3];
   const float* an = W_ANCHOR[W];
@@ -620,7 +628,6 @@ __device__ __forceinline__ int wheel_contacts(const Slots& S, const float p[3], 
 #pragma unroll
   for (int k = 0; k < 3; k++) axis[k] *= CYL_H;
   prjaxis *= CYL_H;
-  int cnt = 0;
   float dpos[4][3], dd[4];
   bool act[4] = {false, false, false, false};
   float d1 = dist0 + prjaxis + prjvec;
@@ -649,30 +656,28 @@ __device__ __forceinline__ int wheel_contacts(const Slots& S, const float p[3], 
       }
     }
   }
+  uint32_t bits = 0;
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     // included in the constraint set only if dist < margin - gap = 0
     bool on = act[t] && dd[t] < 0.0f;
-    S.at(s0 + t, 12) = on ? 1.0f : 0.0f;
     if (on) {
+      bits |= 1u << (s0 + t);
       // midpoint contact position, then chassis-frame point relative to the chassis origin
       float w[3] = {dpos[t][0] - p[0], dpos[t][1] - p[1], dpos[t][2] - 0.5f * dd[t] - p[2]};
       S.at(s0 + t, 0) = R[0] * w[0] + R[3] * w[1] + R[6] * w[2];
       S.at(s0 + t, 1) = R[1] * w[0] + R[4] * w[1] + R[7] * w[2];
       S.at(s0 + t, 2) = R[2] * w[0] + R[5] * w[1] + R[8] * w[2];
       S.at(s0 + t, 3) = dd[t];
-      cnt++;
     }
   }
-  return cnt;
+  return bits;
 }
 
 // plane vs convex hull of welded mesh K: support vertex + up to 3 spread vertices
 template <int K>
-__device__ __forceinline__ int mesh_contacts(const Slots& S, const float p[3], const float R[9]) {
+__device__ __forceinline__ uint32_t mesh_contacts(const Slots& S, const float p[3], const float R[9]) {
   constexpr int s0 = 16 + K * 4;
-#pragma unroll
-  for (int t = 0; t < 4; t++) S.at(s0 + t, 12) = 0.0f;
   // conservative lower bound on the hull's height (chassis-frame AABB)
   float zc = p[2], ext = 0.0f;
 #pragma unroll
@@ -708,7 +713,7 @@ __device__ __forceinline__ int mesh_contacts(const Slots& S, const float p[3], c
     if (pick < 0) break;
     sel[nsel++] = pick;
   }
-  int cnt = 0;
+  uint32_t bits = 0;
   for (int t = 0; t < nsel; t++) {
     int i = sel[t];
     float z = p[2] + R[6] * HULL[K][i][0] + R[7] * HULL[K][i][1] + R[8] * HULL[K][i][2];
@@ -718,10 +723,9 @@ __device__ __forceinline__ int mesh_contacts(const Slots& S, const float p[3], c
     S.at(s0 + t, 1) = HULL[K][i][1] - R[7] * 0.5f * z;
     S.at(s0 + t, 2) = HULL[K][i][2] - R[8] * 0.5f * z;
     S.at(s0 + t, 3) = z;
-    S.at(s0 + t, 12) = 1.0f;
-    cnt++;
+    bits |= 1u << (s0 + t);
   }
-  return cnt;
+  return bits;
 }
 
 #define FOR_CHAINS(F, ...) \
@@ -739,7 +743,7 @@ struct StepResult {
 };
 
 // forward dynamics + constraint solve for one env (state in registers), u coordinates
-__device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
+__device__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
                          const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
   // front steer angles -> spin / cylinder axes in the chassis frame
   float sa[2][3], cyl[2][3];
@@ -750,6 +754,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
     rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
     rot_axis(cyl[s], S_AXIS[s], W_CYL_AXIS[2 + s], c, sn);
   }
+  STAMP(2);
   Solver sv;
   build_M(sv.M, sa);
   float b[NV];
@@ -784,22 +789,28 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
   for (int i = 0; i < NV; i++) sv.a0[i] = sv.fs[i];
   chol12_solve(L, sv.a0);
 
+  STAMP(3);
   // contacts
+  S.lmask = 0u;
   if (flags & F_CONTACTS) {
     const float rear_cyl[3] = {W_CYL_AXIS[0][0], W_CYL_AXIS[0][1], W_CYL_AXIS[0][2]};
     const float rear_cyl1[3] = {W_CYL_AXIS[1][0], W_CYL_AXIS[1][1], W_CYL_AXIS[1][2]};
-    wheel_contacts<0>(S, qpos, R, rear_cyl);
-    wheel_contacts<1>(S, qpos, R, rear_cyl1);
-    wheel_contacts<2>(S, qpos, R, cyl[0]);
-    wheel_contacts<3>(S, qpos, R, cyl[1]);
-    mesh_contacts<0>(S, qpos, R);
-    mesh_contacts<1>(S, qpos, R);
-  } else {
-    slot_deactivate_all(S);
+    S.lmask |= wheel_contacts<0>(S, qpos, R, rear_cyl);
+    S.lmask |= wheel_contacts<1>(S, qpos, R, rear_cyl1);
+    S.lmask |= wheel_contacts<2>(S, qpos, R, cyl[0]);
+    S.lmask |= wheel_contacts<3>(S, qpos, R, cyl[1]);
+    S.lmask |= mesh_contacts<0>(S, qpos, R);
+    S.lmask |= mesh_contacts<1>(S, qpos, R);
   }
+  // wave-uniform union of active slots (24 ballots -> SGPR mask)
+  S.wmask = 0u;
+#pragma unroll
+  for (int b = 0; b < NSLOT; b++)
+    if (__ballot((S.lmask >> b) & 1u)) S.wmask |= 1u << b;
   // contact frame directions in the chassis frame: n = e_z, t1 = e_y, t2 = -e_x (mju_makeFrame)
   float dirs[3][3] = {{R[6], R[7], R[8]}, {R[3], R[4], R[5]}, {-R[0], -R[1], -R[2]}};
 
+  STAMP(4);
   float K, B;
   ref_kb(K, B);
   // scalar rows: jar, D, type, R*floss
@@ -881,9 +892,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
   // slot field 4..7 temporarily = J a_w - aref ; we evaluate cost then re-init for the chosen.
   FOR_CHAINS(slot_loop_init, S, dirs, sa, warm_u, u, K, B);
   float cw_c = 0.0f;
-#pragma unroll 1
-  for (int s = 0; s < NSLOT; s++) {
-    if (S.at(s, 12) == 0.0f) continue;
+  FOR_SLOTS(S, S.wmask, s) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       float x = S.at(s, 4 + r);
@@ -899,9 +908,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
     for (int i = 0; i < NV; i++) dpa[i] = sv.a0[i] - warm_u[i];
     FOR_CHAINS(slot_loop_jp, S, dirs, sa, dpa);
     float cs_c = 0.0f;
-#pragma unroll 1
-    for (int s = 0; s < NSLOT; s++) {
-      if (S.at(s, 12) == 0.0f) continue;
+    FOR_SLOTS(S, S.wmask, s) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         float x = S.at(s, 4 + r) + S.at(s, 8 + r);
@@ -913,9 +920,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = use_w ? warm_u[i] : sv.a0[i];
     if (!use_w) {
-#pragma unroll 1
-      for (int s = 0; s < NSLOT; s++) {
-        if (S.at(s, 12) == 0.0f) continue;
+      FOR_SLOTS(S, S.wmask, s) {
 #pragma unroll
         for (int r = 0; r < 4; r++) S.at(s, 4 + r) += S.at(s, 8 + r);
       }
@@ -925,18 +930,26 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
 #pragma unroll
   for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
 
+  STAMP(5);
   // ---------------- Newton iterations
-  const float scale = 1.0f / (MEANINERTIA * (float)NV);
-  bool done = false;
+  // Converged when the previous step was a full (alpha = 1) Newton step that changed no row
+  // state -- within a fixed active set the cost is quadratic, so that step was exact -- or when
+  // the gradient is at the f32 noise floor of its two cancelling parts (rows flickering at a
+  // region boundary), or after MAXIT iterations.
+  bool exact = false;
+  int it_done = MAXIT, why = 4;
 #pragma unroll 1
   for (int it = 0; it < MAXIT; it++) {
-    if (done) break;
+    if (exact) { it_done = it; if (why != 2) why = 1; break; }
     float H[NV][NV], grad[NV];
+    float gscale = 0.0f;
     {
       float da[NV];
 #pragma unroll
       for (int i = 0; i < NV; i++) da[i] = a[i] - sv.a0[i];
       symv12(sv.M, da, grad);
+#pragma unroll
+      for (int i = 0; i < NV; i++) gscale = fmaxf(gscale, fabsf(grad[i]));
     }
 #pragma unroll
     for (int i = 0; i < NV; i++)
@@ -970,10 +983,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
       }
     }
     FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad);
-    float gn2 = 0.0f;
-#pragma unroll
-    for (int i = 0; i < NV; i++) gn2 += grad[i] * grad[i];
-    if (scale * sqrtf(gn2) < 1e-10f) break;
+    (void)gscale;
     chol12(H);
     float pdir[NV];
 #pragma unroll
@@ -998,9 +1008,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
         int type = r == 0 ? 0 : (r <= 6 ? 1 : 2);
         ls_row(sj[r] + al * sjp[r], sjp[r], sD[r], type, sRfl[r], sfl[r], g, h);
       }
-#pragma unroll 1
-      for (int s = 0; s < NSLOT; s++) {
-        if (S.at(s, 12) == 0.0f) continue;
+      FOR_SLOTS(S, S.wmask, s) {
         float D = S.at(s, 3);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -1010,24 +1018,34 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
         }
       }
     };
-    float g0, h0;
-    dphi(0.0f, g0, h0);
-    if (!(g0 < 0.0f)) break;  // no descent
+    // phi'(0) = grad . p (no row pass needed); try the full Newton step first
+    float g0 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NV; i++) g0 += grad[i] * pdir[i];
+    if (!(g0 < 0.0f)) { it_done = it; why = 3; break; }  // no descent left: optimum to f32 precision
     float lo = 0.0f, hi = 3.0e38f, al = 1.0f;
+    bool full = false;
 #pragma unroll 1
     for (int k = 0; k < LSIT; k++) {
       float g, h;
       dphi(al, g, h);
-      if (fabsf(g) <= 1e-6f * fabsf(g0)) break;
+      if (fabsf(g) <= 1e-4f * fabsf(g0)) { full = (k == 0); break; }
       if (g < 0.0f) lo = al; else hi = al;
       float nal = al - g / h;
       if (!(nal > lo && nal < hi)) nal = (hi < 3.0e38f) ? 0.5f * (lo + hi) : 2.0f * al;
+      bool tiny = fabsf(nal - al) <= 1e-6f * al;
       al = nal;
+      if (tiny) break;
     }
-    // move, count row-state changes (no change at a full Newton step = converged)
+    // move, count row-state changes; "still" = the update is below f32 resolution of a
     int changed = 0;
+    bool still = true;
 #pragma unroll
-    for (int i = 0; i < NV; i++) a[i] += al * pdir[i];
+    for (int i = 0; i < NV; i++) {
+      float d = al * pdir[i];
+      still = still && fabsf(d) <= 2e-6f * fmaxf(fabsf(a[i]), 1.0f);
+      a[i] += d;
+    }
 #pragma unroll
     for (int r = 0; r < NSCAL; r++) {
       float x0 = sj[r], x1 = sj[r] + al * sjp[r];
@@ -1037,9 +1055,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
       }
       sj[r] = x1;
     }
-#pragma unroll 1
-    for (int s = 0; s < NSLOT; s++) {
-      if (S.at(s, 12) == 0.0f) continue;
+    FOR_SLOTS(S, S.wmask, s) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         float x0 = S.at(s, 4 + r), x1 = x0 + al * S.at(s, 8 + r);
@@ -1047,8 +1063,16 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
         S.at(s, 4 + r) = x1;
       }
     }
-    if (changed == 0 && fabsf(al - 1.0f) < 1e-3f) done = true;
+    exact = (full && changed == 0) || still;
+    if (still && !(full && changed == 0)) why = 2;
   }
+  STAMP(6);
+#ifdef AK_STAMPS
+  g_stamps[16 * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] = (unsigned long long)(it_done * 8 + why);
+#else
+  (void)it_done;
+  (void)why;
+#endif
 #pragma unroll
   for (int i = 0; i < NV; i++) out.qacc[i] = a[i];
   // qfrc_constraint = J^T f at the solution
@@ -1084,6 +1108,7 @@ __device__ void dynamics(const Slots& S, const float qpos[13], const float u[NV]
 #pragma unroll
   for (int i = 0; i < NV; i++) bad |= is_bad(a[i]);
   out.bad = bad;
+  STAMP(7);
 }
 
 // ------------------------------------------------------------------ state I/O helpers
@@ -1145,6 +1170,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
   const int e = blockIdx.x * 64 + lane;
   if (e >= A.n) return;
   const int n = A.n;
+  STAMP(0);
   Slots S{lds + lane};
   float* st = A.state;
   float qpos[13], qvel[NV], warm[NV];
@@ -1164,6 +1190,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
   float ctrl[3];
   bool badctrl;
   controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+  STAMP(1);
 
   // mj_checkPos / mj_checkVel: bad state -> mj_resetData (qpos0, zero velocity/warmstart/ctrl)
   bool bad_state = false;
@@ -1198,6 +1225,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     if (res.bad && pass == 0) { bad_state = true; continue; }
 
     // observation / reward on the pre-integration pose
+    STAMP(8);
     const uint32_t nstep = step + 1;
     const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
     float head[7];
@@ -1228,6 +1256,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
       A.info[3 * (size_t)n + e] = bad_state ? 1.0f : 0.0f;
     }
 
+    STAMP(9);
     if (autoreset) {
       reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1, A.prm);
       return;
@@ -1272,6 +1301,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
 #pragma unroll
     for (int i = 0; i < NV; i++) st[(size_t)(ST_WARM + i) * n + e] = warm[i];
     st[(size_t)ST_STEP * n + e] = __uint_as_float(nstep);
+    STAMP(10);
     return;
   }
 }
@@ -1330,6 +1360,13 @@ static uint64_t fnv1a64(const unsigned char* p, size_t n) {
 extern "C" {
 
 const char* ackphys_last_error(void) { return g_err; }
+#ifdef AK_STAMPS
+int ackphys_diag_set_stamps(void* buf) {
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf));
+  return e == hipSuccess ? 0 : hipfail(e, "hipMemcpyToSymbol");
+}
+#endif
+
 const char* ackphys_version(void) { return "ackphys 0.1 (gfx950, lane-per-env)"; }
 uint64_t ackphys_model_fnv(void) { return apg::MODEL_FNV; }
 

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Diagnostic (stamped) build of the step kernel -> csrc/build/libackphys_stamps.so (never loaded by the product)
+set -e
+cd "$(dirname "$0")/../mujoco_playground_amd/csrc"
+mkdir -p build
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -DAK_STAMPS \
+  -o build/libackphys_stamps.so ackphys_step.hip

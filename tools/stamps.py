@@ -1,0 +1,78 @@
+"""Per-phase cycle breakdown of ackphys_step_kernel from the stamped diagnostic build.
+
+    tools/build_diag.sh && python tools/stamps.py
+Phases (stamp k -> k+1): 0 load/controller, 1 kinematics->dynamics entry, 2 M/bias/a0,
+3 contacts, 4 rows+warmstart, 5 Newton, 6 force+Euler solve, 7 (return) -> 8 obs prep,
+8 obs/reward write, 9 integrate+store.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+NAMES = ["controller", "kin->dyn", "M/bias/a0", "contacts", "rows+warm", "newton", "force+euler",
+         "->obs", "obs+reward", "integrate+store"]
+
+
+def main():
+    L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", "libackphys_stamps.so"))
+    P = C.c_void_p
+    L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
+    L.ackphys_step.argtypes = [P] * 10 + [C.c_uint32, C.c_uint64, P]
+    L.ackphys_reset.argtypes = [P, P, C.c_uint64, P, P, P]
+    L.ackphys_random_actions.argtypes = [P, P, C.c_int, C.c_uint64, C.c_uint32, P]
+    L.ackphys_diag_set_stamps.argtypes = [P]
+    blob = open(os.path.join(REPO, "mujoco_playground_amd", "model", "assets", "ackermann_robot_v2.apm"), "rb").read()
+    n = 4096
+    dev = torch.device("cuda:0")
+    ctx = P()
+    assert L.ackphys_create(blob, len(blob), n, 0, C.byref(ctx)) == 0
+    state = torch.zeros(44, n, device=dev)
+    obs = torch.zeros(79, n, device=dev)
+    rew = torch.zeros(n, device=dev)
+    term = torch.zeros(n, dtype=torch.uint8, device=dev)
+    trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nb = (n + 63) // 64
+    stamps = torch.zeros(16 * nb + nb * 64, dtype=torch.int64, device=dev)
+    assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
+    p = lambda t: P(t.data_ptr())
+    stream = P(torch.cuda.current_stream().cuda_stream)
+    acts = torch.zeros(300, n, 2, device=dev)
+    L.ackphys_random_actions(ctx, p(acts), 300, 0, 0, stream)
+    for flags, label in [(2, "contacts OFF"), (3, "contacts ON")]:
+        state.zero_()
+        L.ackphys_reset(ctx, None, 0, p(state), p(obs), stream)
+        for k in range(200):
+            L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
+                           stream)
+        torch.cuda.synchronize()
+        res = []
+        for k in range(200, 210):
+            stamps.zero_()
+            L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
+                           stream)
+            torch.cuda.synchronize()
+            allv = stamps.cpu().numpy()
+            s = allv[: 16 * nb].reshape(16, nb)[:11]
+            res.append(np.diff(s, axis=0))
+            its = allv[16 * nb:]
+            if k == 200:
+                itn, why = its // 8, its % 8
+                wmax = itn.reshape(nb, 64).max(axis=1)
+                print(f"  iterations: lane mean {itn.mean():.2f}, lane hist {np.bincount(itn, minlength=13)}, "
+                      f"wave-max hist {np.bincount(wmax, minlength=13)}, exit reasons (1 exact,2 grad,3 nodesc,4 maxit) "
+                      f"{np.bincount(why, minlength=5)[1:]}")
+        d = np.median(np.concatenate(res, axis=1), axis=1)
+        tot = np.median(np.concatenate([np.sum(r, axis=0) for r in res]))
+        print(f"== {label}: median cycles per wave, total {tot:.0f}")
+        for name, v in zip(NAMES, d):
+            print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
