@@ -105,28 +105,36 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
     n = 4096
     st = np.zeros((n, NSTATE))
     o.reset(st, seed=seed)
-    rng_acts = BatchedAckermannSim(n, device, seed=seed, contacts=contacts).random_actions(400, seed=seed).cpu().numpy()
-    # probe, then size the sample to ~budget_s of CPU work
+    asim = BatchedAckermannSim(n, device, seed=seed, contacts=contacts)
+    # probe a few steps, then size the sample to ~budget_s of CPU work (same Philox action stream)
+    acts = asim.random_actions(8, seed=seed, step0=0).cpu().numpy()
     t0 = time.perf_counter()
-    o.step(st, rng_acts[0], flags=flags, seed=seed, nthreads=threads)
-    probe = time.perf_counter() - t0
-    k = int(max(5, min(399, budget_s / max(probe, 1e-6))))
+    for i in range(8):
+        o.step(st, acts[i], flags=flags, seed=seed, nthreads=threads)
+    probe = (time.perf_counter() - t0) / 8
+    k = int(max(8, min(4000, budget_s / max(probe, 1e-6))))
+    acts = asim.random_actions(k, seed=seed, step0=8).cpu().numpy()
     t0 = time.perf_counter()
-    for i in range(1, k + 1):
-        o.step(st, rng_acts[i], flags=flags, seed=seed, nthreads=threads)
+    for i in range(k):
+        o.step(st, acts[i], flags=flags, seed=seed, nthreads=threads)
     dt = time.perf_counter() - t0
     base = {"value": n * k / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ackphys_oracle.c (f64 restatement of mj_step + env glue), {n} envs x {k} steps "
-                      f"from reset, same Philox actions/flags, OpenMP {threads} threads, {dt:.1f} s"}
+                      f"after 8 probe steps from reset, same Philox actions/flags, OpenMP {threads} threads, {dt:.1f} s"}
     return parity, base
 
 
-def load_traffic(kern_name="ackphys_step_kernel"):
+def load_traffic(contacts: bool, kern_name="ackphys_step_kernel"):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/profile_pmc.py);
+    None if that profile is absent or was taken on another workload."""
     path = os.path.join(HERE, "profiles", "pmc_latest.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kern_name, {}).get("hbm_bytes_per_launch")
+        k = d.get(kern_name, {})
+        if bool(k.get("contacts")) != contacts:
+            return None
+        return k.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -158,7 +166,7 @@ def main():
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
     bpe = algorithmic_bytes_per_env_step()
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic()
+    traffic = load_traffic(contacts)
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
