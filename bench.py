@@ -41,9 +41,9 @@ def algorithmic_bytes_per_env_step() -> int:
     return 176 + 8 + 16 + 152 + 316 + 4 + 2 + 16
 
 
-def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0):
+def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto"):
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
-                              env_offset=shard.env_offset(rank, n_env))
+                              env_offset=shard.env_offset(rank, n_env), variant=variant)
     sim.reset()
     actions = sim.random_actions(warmup + steps, seed=seed)
     for k in range(warmup):
@@ -148,17 +148,19 @@ def main():
     ap.add_argument("--contacts", type=int, default=0, help="0 = configs[1] (default), 1 = configs[2]")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane"], help="step-kernel lane mapping")
     a = ap.parse_args()
     rank, world, local = shard.init()
-    device = torch.device("cuda", local)
+    device = shard.device_for(local)
     torch.cuda.set_device(device)
     contacts = bool(a.contacts)
-    sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device)
+    sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
+                                             variant=a.variant)
     total_envs = a.envs * world
     value = total_envs * a.steps / elapsed
     secondary = None
     if not a.no_secondary:
-        _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device)
+        _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant)
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
                      "kernel_ms": km2}
     parity = base = None
@@ -179,7 +181,9 @@ def main():
                        "parallelism": f"dp{world} (independent env shards, 1 all_gather of episode stats)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ackphys_step_kernel", "kernel_ms": kern_ms,
+                         "kernel": "ackphys_step_quad_kernel" if (a.variant == "quad" or (a.variant == "auto" and contacts))
+                         else "ackphys_step_kernel",
+                         "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_env_step": bpe,
                          "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary,

@@ -74,6 +74,15 @@ typedef struct ackphys_env_params {
 } ackphys_env_params;
 int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
 
+/* Step-kernel mapping: ACKPHYS_VARIANT_QUAD runs each env on 4 lanes of a wavefront (one per
+ * wheel: contacts, Jacobian rows, Hessian/line-search partials, a quarter of the rays);
+ * ACKPHYS_VARIANT_LANE runs each env on one lane; ACKPHYS_VARIANT_AUTO (default) picks QUAD when
+ * contacts are enabled and LANE otherwise. Same results up to f32 summation order. */
+#define ACKPHYS_VARIANT_LANE 0
+#define ACKPHYS_VARIANT_QUAD 1
+#define ACKPHYS_VARIANT_AUTO 2
+int ackphys_set_variant(ackphys_t* ctx, int variant);
+
 /* Global index of this context's env 0 (multi-GPU sharding: rank r passes r*n_env); it keys
  * the Philox streams for goals so a sharded run is identical to an unsharded one. */
 int ackphys_set_env_offset(ackphys_t* ctx, int64_t env_offset);

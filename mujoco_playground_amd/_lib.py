@@ -13,7 +13,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(CSRC, "build", "libackphys.so")
 REPO = os.path.dirname(PKG)
-SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_model_gen.h"),
+SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_quad.inc"),
+           os.path.join(CSRC, "ackphys_model_gen.h"),
            os.path.join(REPO, "include", "ackphys.h"), os.path.join(REPO, "include", "ackphys_model.h")]
 BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
 
@@ -50,7 +51,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     return LIB_PATH
 
 
-EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
+EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
 _lib = None
@@ -72,6 +73,7 @@ def lib():
     L.ackphys_create.argtypes = [C.c_char_p, sz, i32, i32, C.POINTER(P)]
     L.ackphys_destroy.argtypes = [P]
     L.ackphys_set_env_offset.argtypes = [P, i64]
+    L.ackphys_set_variant.argtypes = [P, i32]
     L.ackphys_set_env_params.argtypes = [P, C.POINTER(EnvParams)]
     L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, P, u32, u64, P]
     L.ackphys_reset.argtypes = [P, P, u64, P, P, P]

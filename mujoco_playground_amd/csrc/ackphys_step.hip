@@ -103,7 +103,7 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // ------------------------------------------------------------------ controller (f64)
 // BicycleController.cmd_vel_to_controls + apply_cmd_vel, controller.py:98-140, evaluated in
 // float64 exactly like the reference (its thresholds 1e-6 / 1e-5 sit on f64 values).
-__device__ void controller(float a0f, float a1f, float max_lin, float max_ang, float ctrl[3], bool& bad) {
+__device__ __forceinline__ void controller(float a0f, float a1f, float max_lin, float max_ang, float ctrl[3], bool& bad) {
   // np.clip on the float32 action, then action * max_velocity: float32 x Python float stays
   // float32 under NumPy 2 promotion (ackermann_env.py:190-194); controller works in float64
   a0f = a0f < -1.0f ? -1.0f : (a0f > 1.0f ? 1.0f : a0f);
@@ -163,7 +163,7 @@ __device__ __forceinline__ void rot_axis(float r[3], const float s[3], const flo
 // so only the floor can be hit: mj_ray's plane test with the 40x40 rectangle, cutoff clamp.
 struct ObsOut { float minl, dist, reward; bool term, coll; };
 
-__device__ ObsOut observe_head(const float p[3], const float q[4], const float R[9], float gx, float gy,
+__device__ __forceinline__ ObsOut observe_head(const float p[3], const float q[4], const float R[9], float gx, float gy,
                                const float ref[3], float out8[7], const EnvParams& prm) {
   // odometry (odometry.py:62-103, 154-170)
   float x = p[0] - ref[0], y = p[1] - ref[1];
@@ -194,7 +194,7 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
 }
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
-__device__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
+__device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
                           const float ref[3], float* dst, int n, const EnvParams& prm) {
   float head[7];
   ObsOut o = observe_head(p, q, R, gx, gy, ref, head, prm);
@@ -333,7 +333,7 @@ __device__ __forceinline__ void build_M(float M[NV][NV], const float sa[2][3]) {
 // ------------------------------------------------------------------ bias forces (RNE, u coords)
 // qfrc_bias = Coriolis/centrifugal/gyroscopic + gravity, Newton-Euler per body in the chassis
 // frame with zero generalised acceleration (MuJoCo mj_rne with flg_acc = 0).
-__device__ void bias(const float u[NV], const float R[9], const float sa[2][3], float b[NV]) {
+__device__ __forceinline__ void bias(const float u[NV], const float R[9], const float sa[2][3], float b[NV]) {
   const float w[3] = {u[3], u[4], u[5]};
   // gravity in the chassis frame
   const float g[3] = {R[0] * GRAV[0] + R[3] * GRAV[1] + R[6] * GRAV[2], R[1] * GRAV[0] + R[4] * GRAV[1] + R[7] * GRAV[2],
@@ -743,7 +743,7 @@ struct StepResult {
 };
 
 // forward dynamics + constraint solve for one env (state in registers), u coordinates
-__device__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
+__device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
                          const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
   // front steer angles -> spin / cylinder axes in the chassis frame
   float sa[2][3], cyl[2][3];
@@ -857,14 +857,14 @@ __device__ void dynamics(Slots& S, const float qpos[13], const float u[NV], cons
   // aref of scalar rows is in sj; jar(a) = J a - aref
 
   // warmstart: the cheaper of qacc_warmstart and qacc_smooth (cost = gauss + constraint)
-  auto scal_J_dot = [&](int r, const float x[NV]) -> float {
+  auto scal_J_dot = [&](int r, const float x[NV]) __attribute__((always_inline)) -> float {
     if (r == 0) return x[EQ_DOF1] + eqc2 * x[EQ_DOF2];
     if (r <= 6) return x[5 + r];
     int l = (r - 7) >> 1;
     float c = ((r - 7) & 1) ? -1.0f : 1.0f;
     return c * x[LIM_DOF[l]];
   };
-  auto scal_cost = [&](int r, float x) -> float {
+  auto scal_cost = [&](int r, float x) __attribute__((always_inline)) -> float {
     if (!sact[r]) return 0.0f;
     if (r == 0) return 0.5f * sD[r] * x * x;
     if (r <= 6) {
@@ -999,7 +999,7 @@ __device__ void dynamics(Slots& S, const float qpos[13], const float u[NV], cons
     float pMp = 0.0f, pg0 = 0.0f;
 #pragma unroll
     for (int i = 0; i < NV; i++) { pMp += pdir[i] * Mp[i]; pg0 += Mp[i] * (a[i] - sv.a0[i]); }
-    auto dphi = [&](float al, float& g, float& h) {
+    auto dphi = [&](float al, float& g, float& h) __attribute__((always_inline)) {
       g = pg0 + al * pMp;
       h = pMp;
 #pragma unroll
@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
 }
 
 // reset env e: writes state words + observation
-__device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode,
+__device__ __forceinline__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode,
                           const EnvParams& prm) {
   float qpos[13], qvel[NV], warm[NV];
   reset_pose(qpos, qvel, warm);
@@ -1160,6 +1160,8 @@ __device__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed,
 }
 
 }  // namespace ak
+
+#include "ackphys_quad.inc"
 
 // ====================================================================== kernels
 using namespace ak;
@@ -1198,6 +1200,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
   for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
 #pragma unroll
   for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
+#pragma unroll 1
   for (int pass = 0; pass < 2; pass++) {
     if (bad_state) {
 #pragma unroll
@@ -1339,6 +1342,7 @@ struct ackphys_ctx {
   int device;
   int64_t env_offset;
   ak::EnvParams prm;
+  int variant;  // ACKPHYS_VARIANT_LANE (1 lane/env) or ACKPHYS_VARIANT_QUAD (4 lanes/env)
 };
 
 static thread_local char g_err[512];
@@ -1367,7 +1371,7 @@ int ackphys_diag_set_stamps(void* buf) {
 }
 #endif
 
-const char* ackphys_version(void) { return "ackphys 0.1 (gfx950, lane-per-env)"; }
+const char* ackphys_version(void) { return "ackphys 0.2 (gfx950; step kernels: lane-per-env, quad-per-env)"; }
 uint64_t ackphys_model_fnv(void) { return apg::MODEL_FNV; }
 
 int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device, ackphys_t** out) {
@@ -1390,6 +1394,7 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
   c->device = device;
   c->env_offset = 0;
   c->prm = ak::EnvParams{1000, 0.5f, 0.15f, 1.0f, 1.0f};  // AckermannRobotEnv defaults
+  c->variant = ACKPHYS_VARIANT_AUTO;
   *out = c;
   return ACKPHYS_OK;
 }
@@ -1404,6 +1409,14 @@ int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* p) {
   if (p->max_episode_steps <= 0) return fail(ACKPHYS_EINVAL, "max_episode_steps must be positive");
   ctx->prm = ak::EnvParams{p->max_episode_steps, (float)p->goal_distance_threshold, (float)p->collision_threshold,
                            (float)p->max_linear_velocity, (float)p->max_angular_velocity};
+  return ACKPHYS_OK;
+}
+
+int ackphys_set_variant(ackphys_t* ctx, int variant) {
+  if (!ctx) return fail(ACKPHYS_EINVAL, "ctx is NULL");
+  if (variant != ACKPHYS_VARIANT_LANE && variant != ACKPHYS_VARIANT_QUAD && variant != ACKPHYS_VARIANT_AUTO)
+    return fail(ACKPHYS_EINVAL, "bad variant");
+  ctx->variant = variant;
   return ACKPHYS_OK;
 }
 
@@ -1422,8 +1435,17 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
   if (e != hipSuccess) return hipfail(e, "hipSetDevice");
   ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
              ctx->env_offset};
-  int blocks = (ctx->n_env + 63) / 64;
-  hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  // AUTO: with contacts the quad mapping wins (contact rows dominate and split 4 ways); without
+  // contacts the replicated serial core dominates and one lane per env is marginally faster.
+  const bool quad = ctx->variant == ACKPHYS_VARIANT_QUAD ||
+                    (ctx->variant == ACKPHYS_VARIANT_AUTO && (flags & ACKPHYS_CONTACTS));
+  if (quad) {
+    int blocks = (ctx->n_env + 15) / 16;
+    hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  } else {
+    int blocks = (ctx->n_env + 63) / 64;
+    hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");
   return ACKPHYS_OK;

@@ -20,11 +20,25 @@ def dist_env():
 
 
 def init(backend: str | None = None):
+    """Initialise torch.distributed from torchrun's env. Backend: "nccl" (= RCCL on ROCm) when a
+    GPU is present; ACKPHYS_DIST_BACKEND overrides it (rehearsals of N ranks on one GPU use gloo)."""
     rank, world, local = dist_env()
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend or ("nccl" if torch.cuda.is_available() else "gloo"))
+        backend = backend or os.environ.get("ACKPHYS_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend=backend)
     return rank, world, local
+
+
+def device_for(local_rank: int) -> torch.device:
+    """cuda:<local_rank>; ACKPHYS_DEVICE_OVERRIDE pins every rank to one device (rehearsal only)."""
+    ov = os.environ.get("ACKPHYS_DEVICE_OVERRIDE")
+    return torch.device("cuda", int(ov) if ov is not None else local_rank)
+
+
+def _backend_is_gloo() -> bool:
+    return dist.is_initialized() and dist.get_backend() == "gloo"
 
 
 def env_offset(rank: int, envs_per_rank: int) -> int:
@@ -36,10 +50,12 @@ def gather_episode_stats(episode: torch.Tensor, world: int) -> torch.Tensor:
     -> [world, 4, n] on every rank (one all_gather_into_tensor)."""
     if world == 1:
         return episode.unsqueeze(0).clone()
-    out = torch.empty((world * episode.shape[0],) + tuple(episode.shape[1:]), dtype=episode.dtype,
-                      device=episode.device)
-    dist.all_gather_into_tensor(out, episode.contiguous())
-    return out.view((world,) + tuple(episode.shape))
+    src = episode.contiguous()
+    if _backend_is_gloo() and src.is_cuda:
+        src = src.cpu()
+    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src)
+    return out.view((world,) + tuple(episode.shape)).to(episode.device)
 
 
 def summarize_returns(gathered: torch.Tensor) -> dict:
@@ -52,14 +68,14 @@ def summarize_returns(gathered: torch.Tensor) -> dict:
 def max_over_ranks(x: float, world: int, device) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if _backend_is_gloo() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier(world: int, device=None):
     if world > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and not _backend_is_gloo():
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

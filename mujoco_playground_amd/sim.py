@@ -27,7 +27,7 @@ class BatchedAckermannSim:
     def __init__(self, num_envs: int, device="cuda:0", seed: int = 0, contacts: bool = True,
                  env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
                  goal_distance_threshold: float = 0.5, collision_threshold: float = 0.15,
-                 max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0):
+                 max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0, variant: str = "auto"):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
@@ -43,6 +43,8 @@ class BatchedAckermannSim:
         self.params = _lib.EnvParams(int(max_episode_steps), float(goal_distance_threshold), float(collision_threshold),
                                      float(max_linear_velocity), float(max_angular_velocity))
         _lib.check(L.ackphys_set_env_params(ctx, C.byref(self.params)), "ackphys_set_env_params")
+        self.variant = variant
+        _lib.check(L.ackphys_set_variant(ctx, {"lane": 0, "quad": 1, "auto": 2}[variant]), "ackphys_set_variant")
         f32, u8 = torch.float32, torch.uint8
         d = self.device
         self.state = torch.zeros(NSTATE, self.n, dtype=f32, device=d)

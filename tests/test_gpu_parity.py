@@ -79,16 +79,17 @@ def test_reset_matches_oracle(blob):
     np.testing.assert_allclose(sim.obs_soa.cpu().numpy().T, oobs, atol=1e-5)
 
 
+@pytest.mark.parametrize("variant", ["quad", "lane"])
 @pytest.mark.parametrize("contacts", [True, False])
-def test_teacher_forced_step(blob, contacts):
+def test_teacher_forced_step(blob, contacts, variant):
     n, steps, seed = 256, 150, 11
-    sim = make_sim(n, seed=seed, contacts=contacts)
+    sim = make_sim(n, seed=seed, contacts=contacts, variant=variant)
     sim.reset()
     acts = sim.random_actions(steps, seed=seed)
     o = fresh_oracle(blob)
     flags = (1 if contacts else 0) | 2
     w = teacher_forced(sim, o, acts, steps, flags, seed)
-    print("worst", contacts, w)
+    print("worst", variant, contacts, w)
 
 
 def test_autoreset_truncation_terminal_obs(blob):
@@ -171,12 +172,13 @@ def test_bad_state_resets(blob):
     assert torch.isfinite(sim.state).all()
 
 
-def test_sharding_is_exact():
+@pytest.mark.parametrize("variant", ["quad", "lane"])
+def test_sharding_is_exact(variant):
     """Two half-size shards with env offsets reproduce the unsharded run bit for bit."""
     n, steps, seed = 128, 60, 21
-    full = make_sim(n, seed=seed, max_episode_steps=20)
-    a = make_sim(n // 2, seed=seed, env_offset=0, max_episode_steps=20)
-    b = make_sim(n // 2, seed=seed, env_offset=n // 2, max_episode_steps=20)
+    full = make_sim(n, seed=seed, max_episode_steps=20, variant=variant)
+    a = make_sim(n // 2, seed=seed, env_offset=0, max_episode_steps=20, variant=variant)
+    b = make_sim(n // 2, seed=seed, env_offset=n // 2, max_episode_steps=20, variant=variant)
     for s in (full, a, b):
         s.reset()
     acts_full = full.random_actions(steps, seed=seed)
