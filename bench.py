@@ -97,8 +97,22 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
         eq = max(eq, float(np.abs(s_after[:, 0:13] - s_before[:, 0:13]).max()))
         ev = max(ev, float(np.abs(s_after[:, 13:25] - s_before[:, 13:25]).max()))
         eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs).max()))
+    # free-running drift (not gated): GPU and oracle both run their own state from the
+    # same reset under the same actions; max |dqpos| after 1/10/100 steps
+    fsim = BatchedAckermannSim(parity_envs, device, seed=seed, contacts=contacts)
+    fsim.reset()
+    facts = fsim.random_actions(100, seed=seed)
+    fst = to_f64_state(fsim.state)
+    drift = {}
+    for k in range(100):
+        fsim.step(facts[k], want_info=False)
+        o.step(fst, facts[k].cpu().numpy(), flags=flags, seed=seed)
+        if k + 1 in (1, 10, 100):
+            torch.cuda.synchronize(device)
+            drift[str(k + 1)] = float(np.abs(to_f64_state(fsim.state)[:, 0:13] - fst[:, 0:13]).max())
     parity = {"max_abs_qpos_err": eq, "max_abs_qvel_err": ev, "max_abs_obs_err": eo,
-              "sample": f"{parity_envs} envs x {parity_steps} teacher-forced steps from reset (f32 GPU vs f64 oracle)"}
+              "sample": f"{parity_envs} envs x {parity_steps} teacher-forced steps from reset (f32 GPU vs f64 oracle)",
+              "free_running_qpos_drift": drift}
     if not do_timing:
         return parity, None
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -118,9 +132,29 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
     for i in range(k):
         o.step(st, acts[i], flags=flags, seed=seed, nthreads=threads)
     dt = time.perf_counter() - t0
+    # 1 core, same per-env work on a smaller batch (~3 s)
+    n1 = 256
+    st1 = np.zeros((n1, NSTATE))
+    o.reset(st1, seed=seed)
+    k1 = int(max(4, min(2000, 3.0 / max(probe * n1 / n * threads, 1e-6))))
+    t1 = time.perf_counter()
+    for i in range(k1):
+        o.step(st1, acts[i % k, :n1], flags=flags, seed=seed, nthreads=1)
+    one_core = n1 * k1 / (time.perf_counter() - t1)
+    # BASELINE configs[0]: one env driven step by step from Python, the oracle standing in for
+    # mj_step (the reference's per-env call pattern: one step call per env per step)
+    st0 = np.zeros((1, NSTATE))
+    o.reset(st0, seed=seed)
+    k0, t2 = 2000, time.perf_counter()
+    for i in range(k0):
+        o.step(st0, acts[i % k, :1], flags=flags, seed=seed, nthreads=1)
+    one_env = k0 / (time.perf_counter() - t2)
     base = {"value": n * k / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ackphys_oracle.c (f64 restatement of mj_step + env glue), {n} envs x {k} steps "
-                      f"after 8 probe steps from reset, same Philox actions/flags, OpenMP {threads} threads, {dt:.1f} s"}
+                      f"after 8 probe steps from reset, same Philox actions/flags, OpenMP {threads} threads, {dt:.1f} s",
+            "one_core": {"value": one_core, "sample": f"{n1} envs x {k1} steps, 1 thread"},
+            "config0_python_1env": {"value": one_env, "sample": f"1 env x {k0} steps, one Python call per step "
+                                                                "(BASELINE configs[0] call pattern)"}}
     return parity, base
 
 

@@ -49,6 +49,9 @@ typedef struct ackphys_ctx ackphys_t;
 /* step flags */
 #define ACKPHYS_CONTACTS 1u  /* 0 = MJCF <flag contact="disable"/> (BASELINE config 2) */
 #define ACKPHYS_AUTORESET 2u /* SB3 VecEnv semantics: reset done envs inside the step */
+/* obs/reward from the post-step pose: render_mode="human" runs mj_forward after mj_step
+ * (ackermann_env.py:202-207). Default (flag clear): the pre-integration pose mj_step's sensors see. */
+#define ACKPHYS_POSTSTEP_OBS 4u
 
 /* error codes */
 #define ACKPHYS_OK 0

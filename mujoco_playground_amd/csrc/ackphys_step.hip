@@ -46,7 +46,7 @@ constexpr int NV = 12;
 constexpr int NSTATE = 44;
 constexpr int NOBS = 79;
 constexpr int ST_QPOS = 0, ST_QVEL = 13, ST_WARM = 25, ST_GOAL = 37, ST_REF = 39, ST_STEP = 42, ST_EPIS = 43;
-constexpr uint32_t F_CONTACTS = 1u, F_AUTORESET = 2u;
+constexpr uint32_t F_CONTACTS = 1u, F_AUTORESET = 2u, F_POSTSTEP_OBS = 4u;
 constexpr int NSLOT = 24;        // 4 wheels x 4 + 2 meshes x 4 contact slots
 constexpr int NF = 13;           // Pb[3], D, jar[4], jp[4], active
 constexpr int NSCAL = 11;        // eq(1) + frictionloss(6) + limits(4)
@@ -742,6 +742,58 @@ struct StepResult {
   bool bad;
 };
 
+// mj_Euler + mj_advance: qvel += h acc (u coords -> world linear), positions (free joint: quaternion
+// exponential in the body frame, then normalise), qacc_warmstart <- qacc (back to q coords).
+// R is the pre-integration chassis rotation the u coordinates are expressed in.
+__device__ __forceinline__ void euler_advance(const float u[NV], const StepResult& res, const float R[9],
+                                              float qpos[13], float qvel[NV], float warm[NV]) {
+  float vb[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) vb[k] = u[k] + DT * res.acce[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) qvel[k] = R[3 * k] * vb[0] + R[3 * k + 1] * vb[1] + R[3 * k + 2] * vb[2];
+#pragma unroll
+  for (int i = 3; i < NV; i++) qvel[i] = u[i] + DT * res.acce[i];
+#pragma unroll
+  for (int k = 0; k < 3; k++) qpos[k] += DT * qvel[k];
+  {
+    const float w[3] = {qvel[3], qvel[4], qvel[5]};
+    const float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    float ang = DT * wn;
+    float ax[3];
+    if (wn < MINVAL) { ax[0] = 1; ax[1] = 0; ax[2] = 0; ang = 0; }
+    else { ax[0] = w[0] / wn; ax[1] = w[1] / wn; ax[2] = w[2] / wn; }
+    const float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    const float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
+    float qq[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+    normq(qq);
+    qpos[3] = qq[0] * qr[0] - qq[1] * qr[1] - qq[2] * qr[2] - qq[3] * qr[3];
+    qpos[4] = qq[0] * qr[1] + qq[1] * qr[0] + qq[2] * qr[3] - qq[3] * qr[2];
+    qpos[5] = qq[0] * qr[2] - qq[1] * qr[3] + qq[2] * qr[0] + qq[3] * qr[1];
+    qpos[6] = qq[0] * qr[3] + qq[1] * qr[2] - qq[2] * qr[1] + qq[3] * qr[0];
+  }
+#pragma unroll
+  for (int j = 7; j < 13; j++) qpos[j] += DT * qvel[j - 1];
+#pragma unroll
+  for (int k = 0; k < 3; k++) warm[k] = R[3 * k] * res.qacc[0] + R[3 * k + 1] * res.qacc[1] + R[3 * k + 2] * res.qacc[2];
+#pragma unroll
+  for (int i = 3; i < NV; i++) warm[i] = res.qacc[i];
+}
+
+// Pose the observation is taken at. Default: the pre-integration pose (mj_step's sensors and x*
+// arrays). F_POSTSTEP_OBS: render_mode="human" (ackermann_env.py:202-207) runs mj_forward after
+// mj_step, so obs/reward see the integrated pose.
+__device__ __forceinline__ void obs_pose(uint32_t flags, const float qpos[13], float p[3], float q[4], float R[9]) {
+  if (flags & F_POSTSTEP_OBS) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) p[k] = qpos[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = qpos[3 + k];
+    normq(q);
+    quat_R(q, R);
+  }
+}
+
 // forward dynamics + constraint solve for one env (state in registers), u coordinates
 __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
                          const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
@@ -1227,16 +1279,18 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     dynamics(S, qpos, u, wu, R, ctrl, A.flags, res);
     if (res.bad && pass == 0) { bad_state = true; continue; }
 
-    // observation / reward on the pre-integration pose
     STAMP(8);
+    float p[3] = {qpos[0], qpos[1], qpos[2]};
+    euler_advance(u, res, R, qpos, qvel, warm);
+    obs_pose(A.flags, qpos, p, q, R);
     const uint32_t nstep = step + 1;
     const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
     float head[7];
-    ObsOut oh = observe_head(qpos, q, R, gx, gy, ref, head, A.prm);
+    ObsOut oh = observe_head(p, q, R, gx, gy, ref, head, A.prm);
     const bool done_pre = oh.term || trunc;
     const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
     float* dst = (autoreset && A.tobs) ? A.tobs + e : A.obs + e;
-    ObsOut o = observe(qpos, q, R, gx, gy, ref, dst, n, A.prm);
+    ObsOut o = observe(p, q, R, gx, gy, ref, dst, n, A.prm);
     A.reward[e] = o.reward;
     A.term[e] = o.term ? 1 : 0;
     A.trunc[e] = trunc ? 1 : 0;
@@ -1264,39 +1318,6 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
       reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1, A.prm);
       return;
     }
-    // mj_Euler: qvel += h acc (u coords -> world linear), integrate positions
-    float vb[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) vb[k] = u[k] + DT * res.acce[k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) qvel[k] = R[3 * k] * vb[0] + R[3 * k + 1] * vb[1] + R[3 * k + 2] * vb[2];
-#pragma unroll
-    for (int i = 3; i < NV; i++) qvel[i] = u[i] + DT * res.acce[i];
-#pragma unroll
-    for (int k = 0; k < 3; k++) qpos[k] += DT * qvel[k];
-    {
-      float w[3] = {qvel[3], qvel[4], qvel[5]};
-      float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-      float ang = DT * wn;
-      float ax[3];
-      if (wn < MINVAL) { ax[0] = 1; ax[1] = 0; ax[2] = 0; ang = 0; }
-      else { ax[0] = w[0] / wn; ax[1] = w[1] / wn; ax[2] = w[2] / wn; }
-      float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
-      float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
-      float qq[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
-      normq(qq);
-      qpos[3] = qq[0] * qr[0] - qq[1] * qr[1] - qq[2] * qr[2] - qq[3] * qr[3];
-      qpos[4] = qq[0] * qr[1] + qq[1] * qr[0] + qq[2] * qr[3] - qq[3] * qr[2];
-      qpos[5] = qq[0] * qr[2] - qq[1] * qr[3] + qq[2] * qr[0] + qq[3] * qr[1];
-      qpos[6] = qq[0] * qr[3] + qq[1] * qr[2] - qq[2] * qr[1] + qq[3] * qr[0];
-    }
-#pragma unroll
-    for (int j = 7; j < 13; j++) qpos[j] += DT * qvel[j - 1];
-    // qacc_warmstart <- qacc (back to q coords)
-#pragma unroll
-    for (int k = 0; k < 3; k++) warm[k] = R[3 * k] * res.qacc[0] + R[3 * k + 1] * res.qacc[1] + R[3 * k + 2] * res.qacc[2];
-#pragma unroll
-    for (int i = 3; i < NV; i++) warm[i] = res.qacc[i];
 #pragma unroll
     for (int i = 0; i < 13; i++) st[(size_t)(ST_QPOS + i) * n + e] = qpos[i];
 #pragma unroll

@@ -20,8 +20,9 @@ class AckermannRobotEnv:
     def __init__(self, map_spawner=None, max_episode_steps=1000, goal_distance_threshold=0.5,
                  collision_threshold=0.15, max_linear_velocity=1.0, max_angular_velocity=1.0, render_mode=None,
                  device="cuda:0", contacts: bool = True):
-        if render_mode == "human":
-            raise NotImplementedError("render_mode='human' (MuJoCo viewer) is out of scope (SURVEY.md §2)")
+        # render_mode="human": the reference opens a passive MuJoCo viewer (out of scope here: no
+        # window) and runs mj_forward after every mj_step (ackermann_env.py:202-207), so its
+        # observations/rewards come from the post-step pose. That numerical effect is kept.
         self.max_episode_steps = max_episode_steps
         self.goal_distance_threshold = goal_distance_threshold
         self.collision_threshold = collision_threshold
@@ -34,7 +35,8 @@ class AckermannRobotEnv:
                                         goal_distance_threshold=goal_distance_threshold,
                                         collision_threshold=collision_threshold,
                                         max_linear_velocity=max_linear_velocity,
-                                        max_angular_velocity=max_angular_velocity)
+                                        max_angular_velocity=max_angular_velocity,
+                                        poststep_obs=(render_mode == "human"))
         self._rng = np.random.default_rng()
         self.step_count = 0
         self.goal_position = None

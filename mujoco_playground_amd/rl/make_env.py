@@ -32,5 +32,5 @@ def make_ackermann_env(env_type="maze", maze_id="PointMaze_UMaze-v3", render_mod
     if env_type == "simple":
         return AckermannRobotEnv(render_mode=render_mode, **common, **kwargs)
     if env_type == "vec":
-        return AckermannVecEnv(**common, **kwargs)
+        return AckermannVecEnv(render_mode=render_mode, **common, **kwargs)
     raise ValueError(f"unknown env_type {env_type!r}")

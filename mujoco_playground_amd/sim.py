@@ -13,7 +13,7 @@ import torch
 from . import _lib
 
 NSTATE, NOBS = 44, 79
-CONTACTS, AUTORESET = 1, 2
+CONTACTS, AUTORESET, POSTSTEP_OBS = 1, 2, 4
 
 # state word offsets (include/ackphys.h)
 ST_QPOS, ST_QVEL, ST_WARM, ST_GOAL, ST_REF, ST_STEP, ST_EPIS = 0, 13, 25, 37, 39, 42, 43
@@ -27,13 +27,16 @@ class BatchedAckermannSim:
     def __init__(self, num_envs: int, device="cuda:0", seed: int = 0, contacts: bool = True,
                  env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
                  goal_distance_threshold: float = 0.5, collision_threshold: float = 0.15,
-                 max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0, variant: str = "auto"):
+                 max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0, variant: str = "auto",
+                 poststep_obs: bool = False):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
         self.n = int(num_envs)
         self.seed = int(seed)
         self.contacts = bool(contacts)
+        # render_mode="human" semantics: obs/reward from the post-step pose (ackermann_env.py:202-207)
+        self.poststep_obs = bool(poststep_obs)
         L = _lib.lib()
         blob = model_blob if model_blob is not None else _lib.load_blob()
         ctx = C.c_void_p()
@@ -64,7 +67,7 @@ class BatchedAckermannSim:
 
     @property
     def flags(self) -> int:
-        return CONTACTS if self.contacts else 0
+        return (CONTACTS if self.contacts else 0) | (POSTSTEP_OBS if self.poststep_obs else 0)
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

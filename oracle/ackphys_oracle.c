@@ -31,6 +31,7 @@
 #endif
 
 #include "../include/ackphys_model.h"
+#include "ackphys_oracle.h"
 
 #define mjMINVAL 1e-15
 #define mjMINIMP 0.0001
@@ -52,13 +53,14 @@
 
 #define FLAG_CONTACTS 1u
 #define FLAG_AUTORESET 2u
+#define FLAG_POSTSTEP_OBS 4u /* render_mode="human": mj_forward after mj_step (ackermann_env.py:202-207) */
 
 /* controller constants: controller.py:85-86 */
 #define CTL_WHEEL_R 0.0325
 #define CTL_WHEELBASE 0.20
 #define CTL_TRACK 0.174
 
-typedef struct {
+struct or_ctx {
   const apm_model_t* m;
   const float* mesh_vert;
   const int32_t* mesh_face;
@@ -73,7 +75,7 @@ typedef struct {
   /* resolved ids (reference looks these up by name) */
   int chassis_body, act_steer, act_rl, act_rr;
   int lidar_adr[72];
-} or_ctx;
+};
 
 typedef struct {
   double pos[3], frame[9], dist, friction[5], solref[2], solimp[5], includemargin;
@@ -1429,6 +1431,11 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
   d->ctrl[c->act_rl] = ctrl[1];
   d->ctrl[c->act_rr] = ctrl[2];
   mj_step(c, d, flags);
+  if (flags & FLAG_POSTSTEP_OBS) { /* mj_forward's position stage on the integrated state feeds the obs */
+    kinematics(c, d);
+    com_pos(c, d);
+    sensors(c, d);
+  }
   int t;
   double inf3[3];
   observe(c, d, st + ST_GOAL, st + ST_REF, obs, reward, &t, inf3);
@@ -1543,4 +1550,82 @@ int or_step_diag(const or_ctx* c, const double* st_in, const double* ctrl_in, ui
   memcpy(out + o, d->qvel, sizeof(double) * nv); o += nv;
   free(d);
   return o;
+}
+
+/* ------------------------------------------------------------------ host twin of the C-ABI */
+
+static float f32_of_u32(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static uint32_t u32_of_f32(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+static void soa_to_row(const float* state, int n, int e, double st[NSTATE]) {
+  for (int k = 0; k < NSTATE; k++) st[k] = state[(size_t)k * n + e];
+  st[ST_STEP] = u32_of_f32(state[(size_t)ST_STEP * n + e]);
+  st[ST_EPIS] = u32_of_f32(state[(size_t)ST_EPIS * n + e]);
+}
+static void row_to_soa(const double st[NSTATE], int n, int e, float* state) {
+  for (int k = 0; k < NSTATE; k++) state[(size_t)k * n + e] = (float)st[k];
+  state[(size_t)ST_STEP * n + e] = f32_of_u32((uint32_t)st[ST_STEP]);
+  state[(size_t)ST_EPIS * n + e] = f32_of_u32((uint32_t)st[ST_EPIS]);
+}
+
+/* ackphys_step (include/ackphys.h) on host SoA buffers; episode stats as the kernel keeps them */
+int ackphys_step_cpu(or_ctx* c, int n, const float* action, float* state, float* obs, float* reward,
+                     uint8_t* term, uint8_t* trunc, float* terminal_obs, float* info, float* episode,
+                     uint32_t flags, uint64_t seed, int nthreads) {
+  if (!c || n < 0 || !action || !state || !obs || !reward || !term || !trunc) return -1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+  {
+#endif
+    or_data* d = (or_data*)malloc(sizeof(or_data));
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+    for (int e = 0; e < n; e++) {
+      double st[NSTATE], o[NOBS], to[NOBS], inf[4], r;
+      soa_to_row(state, n, e, st);
+      env_step(c, d, st, action + 2 * (size_t)e, flags, e, seed, o, &r, term + e, trunc + e, to, inf);
+      row_to_soa(st, n, e, state);
+      const int done = term[e] || trunc[e];
+      const double* src = ((flags & FLAG_AUTORESET) && done && terminal_obs) ? to : o;
+      float* dst = ((flags & FLAG_AUTORESET) && done && terminal_obs) ? terminal_obs : obs;
+      for (int k = 0; k < NOBS; k++) dst[(size_t)k * n + e] = (float)src[k];
+      if ((flags & FLAG_AUTORESET) && done && terminal_obs)
+        for (int k = 0; k < NOBS; k++) obs[(size_t)k * n + e] = (float)o[k];
+      reward[e] = (float)r;
+      if (info)
+        for (int k = 0; k < 4; k++) info[(size_t)k * n + e] = (float)inf[k];
+      if (episode) {
+        float ret = episode[e] + (float)r, len = episode[(size_t)n + e] + 1.0f;
+        if (done) {
+          episode[2 * (size_t)n + e] += ret;
+          episode[3 * (size_t)n + e] += 1.0f;
+          ret = 0.0f;
+          len = 0.0f;
+        }
+        episode[e] = ret;
+        episode[(size_t)n + e] = len;
+      }
+    }
+    free(d);
+#ifdef _OPENMP
+  }
+#endif
+  return 0;
+}
+
+int ackphys_reset_cpu(or_ctx* c, int n, const uint8_t* mask, uint64_t seed, float* state, float* obs) {
+  if (!c || n < 0 || !state || !obs) return -1;
+  or_data* d = (or_data*)malloc(sizeof(or_data));
+  for (int e = 0; e < n; e++) {
+    if (mask && !mask[e]) continue;
+    double st[NSTATE], o[NOBS];
+    soa_to_row(state, n, e, st);
+    env_reset(c, d, st, e, seed, o);
+    row_to_soa(st, n, e, state);
+    for (int k = 0; k < NOBS; k++) obs[(size_t)k * n + e] = (float)o[k];
+  }
+  free(d);
+  return 0;
 }

@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libackphys_oracle.so")
 
 NSTATE, NOBS = 44, 79
-FLAG_CONTACTS, FLAG_AUTORESET = 1, 2
+FLAG_CONTACTS, FLAG_AUTORESET, FLAG_POSTSTEP_OBS = 1, 2, 4
 DIAG_LEN = 8192
 
 
@@ -56,6 +56,8 @@ def lib():
         L.or_philox.argtypes = [P, P, P]
         L.or_model_struct_size.restype = i32
         L.or_observe_raw.argtypes = [P, P, P, P, P, P, P, P, P, P]
+        L.ackphys_step_cpu.argtypes = [P, i32] + [P] * 9 + [u32, u64, i32]
+        L.ackphys_reset_cpu.argtypes = [P, i32, P, u64, P, P]
         _lib = L
     return _lib
 

@@ -92,6 +92,16 @@ def test_teacher_forced_step(blob, contacts, variant):
     print("worst", variant, contacts, w)
 
 
+@pytest.mark.parametrize("variant", ["quad", "lane"])
+def test_poststep_obs_mode(blob, variant):
+    """render_mode="human" semantics (mj_forward after mj_step): obs/reward from the integrated pose."""
+    n, steps, seed = 128, 40, 13
+    sim = make_sim(n, seed=seed, contacts=True, variant=variant, poststep_obs=True, max_episode_steps=30)
+    sim.reset()
+    acts = sim.random_actions(steps, seed=seed)
+    teacher_forced(sim, fresh_oracle(blob, max_episode_steps=30), acts, steps, 1 | 2 | 4, seed)
+
+
 def test_autoreset_truncation_terminal_obs(blob):
     n, seed = 64, 3
     sim = make_sim(n, seed=seed, max_episode_steps=25)

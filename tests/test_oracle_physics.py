@@ -149,3 +149,62 @@ def test_quaternion_stays_normalized(oracle):
     for _ in range(300):
         oracle.step(st, rng.uniform(-1, 1, (4, 2)).astype(np.float32))
     assert np.abs(np.linalg.norm(st[:, 3:7], axis=1) - 1).max() < 1e-9
+
+
+def test_poststep_obs_flag_uses_integrated_pose(oracle):
+    """FLAG_POSTSTEP_OBS (render_mode="human"): obs[72:75] = odometry of the *new* qpos; default
+    lags one step (obs of the pre-integration pose)."""
+    from oracle.oracle import FLAG_AUTORESET, FLAG_CONTACTS, FLAG_POSTSTEP_OBS
+    n = 4
+    st = np.zeros((n, 44))
+    oracle.reset(st, seed=3)
+    acts = np.tile(np.array([[0.8, 0.3]], np.float32), (n, 1))
+    for _ in range(200):   # get moving
+        oracle.step(st, acts, flags=FLAG_CONTACTS | FLAG_AUTORESET, seed=3)
+    lag, post = st.copy(), st.copy()
+    obs_lag = oracle.step(lag, acts, flags=FLAG_CONTACTS | FLAG_AUTORESET, seed=3)[0]
+    obs_post = oracle.step(post, acts, flags=FLAG_CONTACTS | FLAG_AUTORESET | FLAG_POSTSTEP_OBS, seed=3)[0]
+    np.testing.assert_array_equal(lag[:, :37], post[:, :37])            # same dynamics
+    np.testing.assert_allclose(obs_lag[:, 72:74], (st[:, 0:2] - st[:, 39:41]).astype(np.float32), atol=1e-6)
+    np.testing.assert_allclose(obs_post[:, 72:74], (post[:, 0:2] - post[:, 39:41]).astype(np.float32), atol=1e-6)
+    assert np.abs(obs_post[:, 72:74] - obs_lag[:, 72:74]).max() > 1e-5
+
+
+def test_step_cpu_twin_matches_row_oracle(blob):
+    """ackphys_step_cpu / ackphys_reset_cpu (oracle/ackphys_oracle.h): the SoA f32
+    host twin of the C-ABI equals the f64 row oracle rounded to f32, including autoreset,
+    terminal obs and the episode-stat words."""
+    import ctypes as C
+    from oracle.oracle import Oracle, lib
+    L = lib()
+    n, seed, flags = 32, 5, 1 | 2
+    oracle = Oracle(blob)
+    oracle.set_env_params(max_episode_steps=12)
+    p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+    state = np.zeros((44, n), np.float32)
+    obs = np.zeros((79, n), np.float32)
+    assert L.ackphys_reset_cpu(oracle._ctx, n, None, seed, p(state), p(obs)) == 0
+    rows = np.zeros((n, 44))
+    robs = oracle.reset(rows, seed=seed)
+    np.testing.assert_array_equal(obs.T, robs.astype(np.float32))
+    rng = np.random.default_rng(0)
+    rew, term, trunc = np.zeros(n, np.float32), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+    tobs, info, ep = np.zeros((79, n), np.float32), np.zeros((4, n), np.float32), np.zeros((4, n), np.float32)
+    for k in range(20):
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        rows = np.ascontiguousarray(state.T, dtype=np.float64)
+        rows[:, 42] = state[42].view(np.uint32)
+        rows[:, 43] = state[43].view(np.uint32)
+        o, r, te, tr, to, inf = oracle.step(rows, act, flags=flags, seed=seed, terminal=True)
+        assert L.ackphys_step_cpu(oracle._ctx, n, p(act), p(state), p(obs), p(rew), p(term), p(trunc), p(tobs),
+                                  p(info), p(ep), flags, seed, 1) == 0
+        np.testing.assert_array_equal(state[:42].T, rows[:, :42].astype(np.float32))
+        np.testing.assert_array_equal(state[42:].view(np.uint32).T, rows[:, 42:].astype(np.uint32))
+        np.testing.assert_array_equal(obs.T, o.astype(np.float32))
+        np.testing.assert_array_equal(rew, r.astype(np.float32))
+        np.testing.assert_array_equal(term.astype(bool), te)
+        np.testing.assert_array_equal(trunc.astype(bool), tr)
+        done = te | tr
+        np.testing.assert_array_equal(tobs.T[done], to[done].astype(np.float32))
+    assert np.all(ep[3] == 1)    # one truncated episode of 12 steps each in 20 steps
+    np.testing.assert_array_equal(ep[1], np.full(n, 8, np.float32))
