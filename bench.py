@@ -68,6 +68,45 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     return sim, elapsed, kern_ms, shard.summarize_returns(gathered), actions
 
 
+def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_epochs=10, seed=0):
+    """BASELINE configs[3]: PPO rollout on the env shard (contacts enabled, SB3 PPO('MlpPolicy')
+    semantics on libackppo.so). One warm-up iteration, then `iters` timed iterations of
+    collect_rollouts (n_steps policy+env steps) + train (n_epochs over minibatches)."""
+    from mujoco_playground_amd.rl import AckermannVecEnv
+    from mujoco_playground_amd.rl.ppo import PPO
+    venv = AckermannVecEnv(n_env, device=device, seed=seed, contacts=True, env_offset=shard.env_offset(rank, n_env))
+    model = PPO("MlpPolicy", venv, n_steps=n_steps, batch_size=batch_size, n_epochs=n_epochs, seed=seed,
+                ent_coef=0.0, world=world, rank=rank)
+    model.collect_rollouts()
+    model.train()
+    stream = torch.cuda.current_stream(device)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2 * iters + 1)]
+    torch.cuda.synchronize(device)
+    shard.barrier(world, device)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    e[0].record(stream)
+    for i in range(iters):
+        model.collect_rollouts()
+        e[2 * i + 1].record(stream)
+        model.train()
+        e[2 * i + 2].record(stream)
+    torch.cuda.synchronize(device)
+    shard.barrier(world, device)
+    el = shard.max_over_ranks(time.perf_counter() - t0, world, device)
+    roll_ms = sum(e[2 * i].elapsed_time(e[2 * i + 1]) for i in range(iters)) / iters
+    train_ms = sum(e[2 * i + 1].elapsed_time(e[2 * i + 2]) for i in range(iters)) / iters
+    steps = iters * n_steps * n_env * world
+    nmb = (n_steps * n_env + batch_size - 1) // batch_size
+    return {"value": steps / el, "unit": "env-steps/s (rollout + update, all ranks)",
+            "rollout_env_steps_per_s": n_steps * n_env * world / (roll_ms * 1e-3),
+            "rollout_ms": roll_ms, "update_ms": train_ms, "minibatch_updates_per_iter": nmb * n_epochs,
+            "update_us_per_minibatch": train_ms * 1e3 / (nmb * n_epochs),
+            "config": f"{n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} ranks, "
+                      f"{n_epochs} epochs, contacts on, {iters} timed iterations after 1 warm-up",
+            "last_logger": {k: v for k, v in model.logger.items() if isinstance(v, (int, float)) or v is None}}
+
+
 def to_f64_state(st: torch.Tensor) -> np.ndarray:
     s = st.detach().cpu().numpy().T.copy()
     out = s.astype(np.float64)
@@ -176,13 +215,14 @@ def load_traffic(contacts: bool, kern_name="ackphys_step_kernel"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--contacts", type=int, default=0, help="0 = configs[1] (default), 1 = configs[2]")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane"], help="step-kernel lane mapping")
+    ap.add_argument("--no-ppo", action="store_true", help="skip the PPO-rollout leg (BASELINE configs[3])")
     a = ap.parse_args()
     rank, world, local = shard.init()
     device = shard.device_for(local)
@@ -197,6 +237,7 @@ def main():
         _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant)
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
                      "kernel_ms": km2}
+    ppo = None if a.no_ppo else run_ppo(a.envs, rank, world, device)
     parity = base = None
     if rank == 0 and not a.no_cpu:
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
@@ -220,7 +261,7 @@ def main():
                          "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_env_step": bpe,
                          "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
-            "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary,
+            "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,0 +1,121 @@
+/* ackppo.h -- C-ABI of libackppo.so: the on-device PPO learner that consumes the batched
+ * Ackermann env (BASELINE configs[3], "PPO rollout").
+ *
+ * It restates what the reference trains with (src/rl/train.py:99-128, 175-179; the stored
+ * hyper-parameters in the rl_logs/ppo checkpoints' data file): stable-baselines3 2.7.0 PPO('MlpPolicy'), i.e.
+ *   ActorCriticPolicy: separate 79-64-64 tanh MLPs for actor and critic, action_net 64->2,
+ *   value_net 64->1, a state-independent log_std [2]; DiagGaussian actions, clipped to the
+ *   action Box before env.step (stored unclipped); GAE(lambda) with the TimeLimit bootstrap
+ *   (reward += gamma * V(terminal_obs) on truncation); per-minibatch advantage
+ *   normalisation; loss = clipped surrogate + vf_coef * MSE(returns, V) - ent_coef * entropy;
+ *   global grad-norm clipping (max_grad_norm); Adam (torch semantics, eps 1e-5).
+ * SB3 is not installed here; the parity oracle is oracle/ppo_oracle.py (numpy float64),
+ * itself cross-checked against torch autograd on the CPU (tests/test_ppo_oracle.py).
+ *
+ * Parameters live in ONE flat float32 vector: the SB3 state_dict tensors (policy.pth key
+ * names, parameters() order), each starting at a multiple of 4 floats (ACKPPO_OFF_*); pad
+ * words are zero. Gradients, Adam moments and gradient partials share the layout.
+ *
+ * Conventions (as include/ackphys.h): DEVICE pointers owned by the caller; work is enqueued
+ * on `stream` (hipStream_t as void*, NULL = default); nothing allocates or synchronises;
+ * 0 = success, negative = error (message via ackppo_last_error()).
+ *
+ * Sample index s = t * n_env + e for rollout step t and env e; every [T][N] buffer is laid
+ * out that way, obs_rows is [T*N][79] (row per sample, gathered by minibatch index).
+ */
+#ifndef ACKPPO_H
+#define ACKPPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACKPPO_NOBS 79
+#define ACKPPO_NACT 2
+#define ACKPPO_HIDDEN 64
+/* flat parameter layout (floats) -- policy.pth keys */
+#define ACKPPO_OFF_LOG_STD 0      /* log_std                          [2]     */
+#define ACKPPO_OFF_PI_W1 4        /* mlp_extractor.policy_net.0.weight [64][79] */
+#define ACKPPO_OFF_PI_B1 5060     /* mlp_extractor.policy_net.0.bias   [64]    */
+#define ACKPPO_OFF_PI_W2 5124     /* mlp_extractor.policy_net.2.weight [64][64] */
+#define ACKPPO_OFF_PI_B2 9220     /* mlp_extractor.policy_net.2.bias   [64]    */
+#define ACKPPO_OFF_VF_W1 9284     /* mlp_extractor.value_net.0.weight  [64][79] */
+#define ACKPPO_OFF_VF_B1 14340    /* mlp_extractor.value_net.0.bias    [64]    */
+#define ACKPPO_OFF_VF_W2 14404    /* mlp_extractor.value_net.2.weight  [64][64] */
+#define ACKPPO_OFF_VF_B2 18500    /* mlp_extractor.value_net.2.bias    [64]    */
+#define ACKPPO_OFF_ACT_W 18564    /* action_net.weight                 [2][64]  */
+#define ACKPPO_OFF_ACT_B 18692    /* action_net.bias                   [2]     */
+#define ACKPPO_OFF_VAL_W 18696    /* value_net.weight                  [1][64]  */
+#define ACKPPO_OFF_VAL_B 18760    /* value_net.bias                    [1]     */
+#define ACKPPO_NPARAM 18764
+#define ACKPPO_TILE 64            /* samples per ackppo_grad workgroup (one partial row each) */
+#define ACKPPO_NLOSS 8            /* loss partial words per workgroup (see ackppo_grad) */
+
+#define ACKPPO_OK 0
+#define ACKPPO_EINVAL -1
+#define ACKPPO_EHIP -3
+
+/* Rollout policy step (SB3 collect_rollouts: policy(obs) -> actions, values, log_probs):
+ * obs_soa [79][n] (ackphys_step's obs buffer). Gaussian noise: Philox4x32-10, key = seed,
+ * counter = (env_offset + e, step, 2, 0), Box-Muller on the first two words.
+ * deterministic != 0: action = mean (predict(deterministic=True)).
+ * Outputs: action [n][2] unclipped sample, env_action [n][2] clipped to [-1,1] (what env.step
+ * receives), log_prob [n], value [n], obs_rows [n][79] copy of the observation (rollout
+ * buffer rows). Every output except env_action may be NULL. */
+int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env_offset, uint64_t seed,
+               uint32_t step, int deterministic, float* obs_rows, float* action, float* env_action,
+               float* log_prob, float* value, void* stream);
+
+/* value [n] = critic(obs_soa) (SB3 policy.predict_values; last_values of a rollout). */
+int ackppo_value(const float* params, const float* obs_soa, int n_env, float* value, void* stream);
+
+/* After one ackphys_step with auto-reset (SB3 collect_rollouts truncation bootstrap):
+ * reward_out[e] = reward[e] + gamma * V(terminal_obs[:, e]) if trunc[e] && !term[e], else reward[e];
+ * done_out[e] = term[e] || trunc[e] (float 0/1: the next step's episode_start). */
+int ackppo_bootstrap(const float* params, const float* terminal_obs_soa, const float* reward, const uint8_t* term,
+                     const uint8_t* trunc, int n_env, float gamma, float* reward_out, float* done_out, void* stream);
+
+/* RolloutBuffer.compute_returns_and_advantage: GAE over T steps, all [T][n].
+ * episode_starts[t] = done flag of step t-1; last_values/last_dones are the state after step T-1. */
+int ackppo_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
+               const float* last_dones, int T, int n_env, float gamma, float gae_lambda, float* advantages,
+               float* returns, void* stream);
+
+/* Per-minibatch advantage statistics for one epoch: minibatch m covers idx[m*batch ..
+ * min((m+1)*batch, n_idx)). stats[m] = (mean, 1/(std+1e-8)) with the unbiased std; (0, 1)
+ * when normalize == 0 or the minibatch has one sample (SB3: len(advantages) > 1). */
+int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int batch, int normalize,
+                     float* stats, void* stream);
+
+/* Gradient of the PPO loss of one minibatch (samples idx[0..batch)), split over
+ * ceil(batch / ACKPPO_TILE) workgroups, each writing its row of grad_partial [nblk][NPARAM]
+ * (pad words are never written: zero them once) and loss_partial [nblk][8] =
+ * (sum pg_loss, sum (R-V)^2, n clipped, sum approx_kl, n samples, 0, 0, 0).
+ * stats: (mean, inv_std) of this minibatch (ackppo_adv_stats). The entropy term is
+ * sample-independent and is added by ackppo_reduce. */
+int ackppo_grad(const float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
+                const float* advantages, const float* returns, const int32_t* idx, int batch, const float* stats,
+                float clip_range, float ent_coef, float vf_coef, float* grad_partial, float* loss_partial,
+                void* stream);
+
+/* grad [NPARAM] = sum of nblk partial rows; d(-ent_coef * entropy)/d log_std = -ent_coef added;
+ * loss [8] = column sums of loss_partial. */
+int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+                  float* loss, void* stream);
+
+/* clip_grad_norm_(max_grad_norm) + torch.optim.Adam step on grad * grad_scale (grad_scale =
+ * 1/world after an all-reduce SUM). step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t)
+ * (host-computed in float64 as torch does). grad_norm_out [1] (nullable): pre-clip norm. */
+int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
+                float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
+                float* grad_norm_out, void* stream);
+
+const char* ackppo_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

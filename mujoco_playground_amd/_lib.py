@@ -17,6 +17,8 @@ SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_q
            os.path.join(CSRC, "ackphys_model_gen.h"),
            os.path.join(REPO, "include", "ackphys.h"), os.path.join(REPO, "include", "ackphys_model.h")]
 BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
+PPO_LIB_PATH = os.path.join(CSRC, "build", "libackppo.so")
+PPO_SOURCES = [os.path.join(CSRC, "ackppo.hip"), os.path.join(REPO, "include", "ackppo.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-fast-math",
                "-Wno-unused-result"]
@@ -33,28 +35,38 @@ class EnvParams(C.Structure):
                 ("max_angular_velocity", C.c_double)]
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
-    """Compile csrc/ackphys_step.hip for gfx950 into csrc/build/libackphys.so (in-tree)."""
-    if not force and os.path.exists(LIB_PATH):
-        t = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(s) <= t for s in SOURCES):
-            return LIB_PATH
-    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+def _hipcc(out: str, sources: list, verbose: bool, force: bool) -> str:
+    if not force and os.path.exists(out):
+        t = os.path.getmtime(out)
+        if all(os.path.getmtime(s) <= t for s in sources):
+            return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "ackphys_step.hip")]
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", out + ".tmp", sources[0]]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    os.replace(out + ".tmp", out)
     if verbose:
-        print(f"built {LIB_PATH}")
-    return LIB_PATH
+        print(f"built {out}")
+    return out
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    """Compile the HIP sources for gfx950 into csrc/build/ (in-tree): libackphys.so (physics
+    step, include/ackphys.h) and libackppo.so (PPO learner, include/ackppo.h)."""
+    _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force)
+    return _hipcc(LIB_PATH, SOURCES, verbose, force)
 
 
 EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
+PPO_EXPORTS = ["ackppo_act", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats", "ackppo_grad",
+               "ackppo_reduce", "ackppo_adam", "ackppo_last_error"]
+
 _lib = None
+_ppo = None
 
 
 def lib():
@@ -83,6 +95,37 @@ def lib():
     L.ackphys_version.restype = C.c_char_p
     _lib = L
     return L
+
+
+def ppo_lib():
+    """The PPO learner C-ABI (libackppo.so); raises ExtensionMissing if the HIP build is absent."""
+    global _ppo
+    if _ppo is not None:
+        return _ppo
+    if not os.path.exists(PPO_LIB_PATH):
+        raise ExtensionMissing(f"{PPO_LIB_PATH} not found: build it with `python -c \"import __graft_entry__ as g; "
+                               f"g.build()\"` (hipcc --offload-arch=gfx950)")
+    try:
+        L = C.CDLL(PPO_LIB_PATH)
+    except OSError as e:
+        raise ExtensionMissing(f"cannot load {PPO_LIB_PATH}: {e}") from e
+    P, i32, i64, u32, u64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
+    L.ackppo_act.argtypes = [P, P, i32, i64, u64, u32, i32, P, P, P, P, P, P]
+    L.ackppo_value.argtypes = [P, P, i32, P, P]
+    L.ackppo_bootstrap.argtypes = [P, P, P, P, P, i32, f32, P, P, P]
+    L.ackppo_gae.argtypes = [P, P, P, P, P, i32, i32, f32, f32, P, P, P]
+    L.ackppo_adv_stats.argtypes = [P, P, i32, i32, i32, P, P]
+    L.ackppo_grad.argtypes = [P, P, P, P, P, P, P, i32, P, f32, f32, f32, P, P, P]
+    L.ackppo_reduce.argtypes = [P, P, i32, f32, P, P, P]
+    L.ackppo_adam.argtypes = [P, P, P, P, f32, f32, f32, f32, f32, f32, f32, P, P]
+    L.ackppo_last_error.restype = C.c_char_p
+    _ppo = L
+    return L
+
+
+def ppo_check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {ppo_lib().ackppo_last_error().decode()}")
 
 
 def load_blob() -> bytes:

@@ -79,3 +79,28 @@ def barrier(world: int, device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+def all_reduce_sum_(t: torch.Tensor, world: int) -> torch.Tensor:
+    """In-place SUM over ranks (RCCL on device; gloo rehearsals go through host memory)."""
+    if world == 1:
+        return t
+    if _backend_is_gloo() and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t)
+    return t
+
+
+def broadcast_(t: torch.Tensor, world: int, src: int = 0) -> torch.Tensor:
+    if world == 1:
+        return t
+    if _backend_is_gloo() and t.is_cuda:
+        h = t.cpu()
+        dist.broadcast(h, src)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src)
+    return t

@@ -42,7 +42,8 @@ class BatchedAckermannSim:
         ctx = C.c_void_p()
         _lib.check(L.ackphys_create(blob, len(blob), self.n, self.device.index or 0, C.byref(ctx)), "ackphys_create")
         self._ctx = ctx
-        _lib.check(L.ackphys_set_env_offset(ctx, int(env_offset)), "ackphys_set_env_offset")
+        self.env_offset = int(env_offset)
+        _lib.check(L.ackphys_set_env_offset(ctx, self.env_offset), "ackphys_set_env_offset")
         self.params = _lib.EnvParams(int(max_episode_steps), float(goal_distance_threshold), float(collision_threshold),
                                      float(max_linear_velocity), float(max_angular_velocity))
         _lib.check(L.ackphys_set_env_params(ctx, C.byref(self.params)), "ackphys_set_env_params")

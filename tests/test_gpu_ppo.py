@@ -1,0 +1,171 @@
+"""GPU parity of libackppo.so (include/ackppo.h) against oracle/ppo_oracle.py (numpy f64).
+
+Tolerances (f32 kernels vs f64 oracle): forward/log_prob/value rel 1e-5 (abs 1e-5), gradient
+rel 2e-4 of the gradient's max magnitude per tensor, Adam-updated parameters abs 1e-7 (the step
+is lr-scaled), GAE rel 1e-5. Discrete outputs (done flags, minibatch counts) exact.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_oracle as po
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def P(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def L():
+    from mujoco_playground_amd import _lib
+    return _lib.ppo_lib()
+
+
+def S():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def params_dev(seed=1):
+    from test_ppo_oracle import _random_params
+    flat = _random_params(seed)
+    return flat, torch.tensor(flat, dtype=torch.float32, device=DEV)
+
+
+def test_act_matches_oracle():
+    flat, p = params_dev()
+    n = 300
+    rng = np.random.default_rng(0)
+    obs = rng.normal(0, 2, (n, 79)).astype(np.float32)
+    soa = torch.tensor(obs.T.copy(), device=DEV)
+    rows = torch.zeros(n, 79, device=DEV)
+    act, eact, lp, val = (torch.zeros(n, 2, device=DEV), torch.zeros(n, 2, device=DEV), torch.zeros(n, device=DEV),
+                          torch.zeros(n, device=DEV))
+    f32 = flat.astype(np.float32).astype(np.float64)
+    for det in (0, 1):
+        assert L().ackppo_act(P(p), P(soa), n, 1000, 0xABCDEF12345, 17, det, P(rows), P(act), P(eact), P(lp), P(val),
+                              S()) == 0
+        torch.cuda.synchronize()
+        a, ea, olp, ov = po.act(f32, obs.astype(np.float64), 0xABCDEF12345, 17, 1000, deterministic=bool(det))
+        np.testing.assert_allclose(act.cpu().numpy(), a, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(eact.cpu().numpy(), ea, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(lp.cpu().numpy(), olp, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(val.cpu().numpy(), ov, rtol=1e-5, atol=2e-5)
+        np.testing.assert_array_equal(rows.cpu().numpy(), obs)
+    vv = torch.zeros(n, device=DEV)
+    assert L().ackppo_value(P(p), P(soa), n, P(vv), S()) == 0
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(vv.cpu().numpy(), ov, rtol=1e-5, atol=2e-5)
+
+
+def test_checkpoint_policy_on_gpu():
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "ppo_policy.npz"))
+    for k in (10000, 20000, 30000):
+        p = torch.tensor(d[f"params_{k}"], device=DEV)
+        soa = torch.tensor(d[f"obs_{k}"].reshape(79, 1).astype(np.float32), device=DEV)
+        ea, a, v = torch.zeros(1, 2, device=DEV), torch.zeros(1, 2, device=DEV), torch.zeros(1, device=DEV)
+        assert L().ackppo_act(P(p), P(soa), 1, 0, 0, 0, 1, None, P(a), P(ea), None, P(v), S()) == 0
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(a.cpu().numpy()[0], d[f"mu_{k}"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(v.item(), d[f"value_{k}"][0], rtol=1e-5)
+
+
+def test_bootstrap_and_gae_match_oracle():
+    flat, p = params_dev(2)
+    n, T = 257, 9
+    rng = np.random.default_rng(1)
+    tobs = rng.normal(0, 1, (n, 79)).astype(np.float32)
+    rew = rng.normal(0, 1, n).astype(np.float32)
+    term = (rng.random(n) < 0.2).astype(np.uint8)
+    trunc = (rng.random(n) < 0.3).astype(np.uint8)
+    ro, do = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    assert L().ackppo_bootstrap(P(p), P(torch.tensor(tobs.T.copy(), device=DEV)), P(torch.tensor(rew, device=DEV)),
+                                P(torch.tensor(term, device=DEV)), P(torch.tensor(trunc, device=DEV)), n, 0.99, P(ro),
+                                P(do), S()) == 0
+    torch.cuda.synchronize()
+    r_ref, d_ref = po.bootstrap(flat.astype(np.float32).astype(np.float64), tobs, rew, term, trunc, 0.99)
+    np.testing.assert_allclose(ro.cpu().numpy(), r_ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(do.cpu().numpy(), d_ref)
+    R, V = rng.normal(size=(T, n)).astype(np.float32), rng.normal(size=(T, n)).astype(np.float32)
+    ST = (rng.random((T, n)) < 0.1).astype(np.float32)
+    lv, ld = rng.normal(size=n).astype(np.float32), (rng.random(n) < 0.2).astype(np.float32)
+    adv, ret = torch.zeros(T, n, device=DEV), torch.zeros(T, n, device=DEV)
+    t = lambda a: torch.tensor(a, device=DEV)
+    assert L().ackppo_gae(P(t(R)), P(t(V)), P(t(ST)), P(t(lv)), P(t(ld)), T, n, 0.99, 0.95, P(adv), P(ret), S()) == 0
+    torch.cuda.synchronize()
+    a_ref, r_ref = po.gae(R.astype(np.float64), V.astype(np.float64), ST, lv, ld, 0.99, 0.95)
+    np.testing.assert_allclose(adv.cpu().numpy(), a_ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret.cpu().numpy(), r_ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("batch,ent_coef", [(64, 0.0), (200, 0.01), (1, 0.0), (4096, 0.0)])
+def test_minibatch_gradient_and_adam_match_oracle(batch, ent_coef):
+    flat, p = params_dev(3)
+    f32 = flat.astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(batch)
+    S_ = 5000
+    obs = rng.normal(0, 1.5, (S_, 79)).astype(np.float32)
+    f = po.forward(f32, obs)
+    acts = (f["mu"] + np.exp(f["log_std"]) * rng.normal(0, 1, (S_, 2))).astype(np.float32)
+    old = (po.log_prob(f["mu"], f["log_std"], acts.astype(np.float64)) + rng.normal(0, 0.3, S_)).astype(np.float32)
+    adv = rng.normal(0.3, 2.0, S_).astype(np.float32)
+    ret = (f["value"] + rng.normal(0, 1, S_)).astype(np.float32)
+    idx = rng.permutation(S_)[:batch].astype(np.int32)
+    t = lambda a: torch.tensor(a, device=DEV)
+    stats = torch.zeros(1, 2, device=DEV)
+    assert L().ackppo_adv_stats(P(t(adv)), P(t(idx)), batch, batch, 1, P(stats), S()) == 0
+    nblk = (batch + 63) // 64
+    gpart, lpart = torch.zeros(nblk, po.NPARAM, device=DEV), torch.zeros(nblk, 8, device=DEV)
+    grad, loss = torch.zeros(po.NPARAM, device=DEV), torch.zeros(8, device=DEV)
+    assert L().ackppo_grad(P(p), P(t(obs)), P(t(acts)), P(t(old)), P(t(adv)), P(t(ret)), P(t(idx)), batch, P(stats),
+                           0.2, ent_coef, 0.5, P(gpart), P(lpart), S()) == 0
+    assert L().ackppo_reduce(P(gpart), P(lpart), nblk, ent_coef, P(grad), P(loss), S()) == 0
+    torch.cuda.synchronize()
+    st, g_ref = po.loss_and_grad(f32, obs[idx].astype(np.float64), acts[idx].astype(np.float64),
+                                 old[idx].astype(np.float64), adv[idx].astype(np.float64), ret[idx].astype(np.float64),
+                                 0.2, ent_coef, 0.5)
+    g = grad.cpu().numpy().astype(np.float64)
+    for k, (o, s) in po.LAYOUT.items():
+        n_ = int(np.prod(s))
+        scale = max(np.abs(g_ref[o:o + n_]).max(), 1e-6)
+        err = np.abs(g[o:o + n_] - g_ref[o:o + n_]).max() / scale
+        assert err < 2e-4, f"{k}: rel err {err:.2e}"
+    lo = loss.cpu().numpy()
+    assert lo[4] == batch
+    np.testing.assert_allclose(lo[0] / batch, st["policy_gradient_loss"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(lo[1] / batch, st["value_loss"], rtol=1e-4)
+    # Adam + clip on the same gradient
+    m, v, norm_out = torch.zeros(po.NPARAM, device=DEV), torch.zeros(po.NPARAM, device=DEV), torch.zeros(1, device=DEV)
+    p2 = p.clone()
+    assert L().ackppo_adam(P(p2), P(grad), P(m), P(v), 1.0, 0.5, 0.9, 0.999, 1e-5, 3e-4 / 0.1, (1 - 0.999) ** 0.5,
+                           P(norm_out), S()) == 0
+    torch.cuda.synchronize()
+    new_ref, _, _, norm_ref = po.clip_and_adam(f32, g, np.zeros(po.NPARAM), np.zeros(po.NPARAM), 1)
+    np.testing.assert_allclose(norm_out.item(), norm_ref, rtol=1e-5)
+    np.testing.assert_allclose(p2.cpu().numpy(), new_ref, atol=1e-7)
+
+
+def test_ppo_learn_end_to_end():
+    """PPO.learn on the batched env: Adam step structure, finite state, surrogate improves."""
+    from mujoco_playground_amd.rl import make_ackermann_env
+    from mujoco_playground_amd.rl.ppo import PPO
+    venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
+    model = PPO("MlpPolicy", venv, n_steps=32, batch_size=1024, n_epochs=4, seed=3, ent_coef=0.01)
+    model.learn(total_timesteps=3 * 32 * 256)
+    assert model.adam_step == 3 * 4 * (32 * 256 // 1024)
+    assert model.num_timesteps == 3 * 32 * 256
+    assert torch.isfinite(model.params).all()
+    lg = model.logger
+    assert np.isfinite(lg["train/value_loss"]) and 0.0 <= lg["train/clip_fraction"] <= 1.0
+    assert lg["rollout/episodes_total"] >= 256  # every env truncated at 64 steps at least once in 96
+    a, _ = model.predict(venv.sim.obs_soa.t(), deterministic=True)
+    assert a.shape == (256, 2) and float(a.abs().max()) <= 1.0
