@@ -8,9 +8,10 @@
 //    workgroups; weights are read with wave-uniform addresses (scalar loads through the
 //    constant cache, FMA with an SGPR operand), hidden activations live in a per-lane LDS
 //    column so the unit loop stays rolled.
-//  * update (ackppo_grad): one 128-lane workgroup per 64-sample tile. Wave 0 runs the actor,
-//    wave 1 the critic, one lane per sample: forward, loss gradient, backward to the hidden
-//    layers, all activations/deltas staged in LDS tiles [unit][sample]. Both waves then form
+//  * update (ackppo_grad): one 256-lane workgroup per 64-sample tile, lane = sample. Waves 0-1
+//    run the actor, waves 2-3 the critic, each on half of the hidden units: forward, loss
+//    gradient, backward to the hidden layers, all activations/deltas staged in LDS tiles
+//    [unit][sample]. All four waves then form
 //    the weight gradients (sums over the tile of outer products) as 4x4 register blocks fed
 //    by 16-B LDS reads along the sample axis, and write the tile's partial gradient row.
 //    ackppo_reduce sums the rows (coalesced over parameters); ackppo_adam applies the global
@@ -137,27 +138,103 @@ struct ActArgs {
   float* value;
 };
 
-extern "C" __global__ void __launch_bounds__(64) ackppo_act_kernel(ActArgs A) {
-  __shared__ float cols[2 * H * 64];
-  const int lane = threadIdx.x, e = blockIdx.x * 64 + lane;
-  if (e >= A.n) return;  // no barriers below: each lane owns its LDS columns
-  float* c1 = cols + lane;
-  float* c2 = cols + H * 64 + lane;
-  float x[NOBS];
-  load_obs_soa(A.obs, A.n, e, x);
-  if (A.obs_rows) {
+// Policy tile: 64 envs (lane = env) x 4 waves. The whole parameter vector is staged in LDS once
+// per workgroup (wide coalesced loads) and read back with wave-uniform addresses (LDS broadcast).
+// Waves split the hidden units: wave w computes units [32w, 32w+32) of the concatenated
+// actor|critic layers (waves 0-1 actor, 2-3 critic), activations exchanged through LDS tiles
+// H1/H2 [128 units][64 envs].
+constexpr int PT_ENVS = 64, PT_THREADS = 256;
+struct PolicyLds {
+  float w[P];
+  float h1[2 * H * PT_ENVS];
+  float h2[2 * H * PT_ENVS];
+};
+
+__device__ __forceinline__ void stage_params(const float* __restrict__ p, float* w) {
+  const float4* src = reinterpret_cast<const float4*>(p);
+  float4* dst = reinterpret_cast<float4*>(w);
+#pragma unroll 4
+  for (int i = threadIdx.x; i < P / 4; i += PT_THREADS) dst[i] = src[i];
+}
+
+// trunks of both nets for the tile; leaves H2 in LDS (caller syncs after)
+__device__ __forceinline__ void policy_trunks(PolicyLds& L, const float (&x)[NOBS], int lane, int wave,
+                                              bool actor, bool critic) {
+  const bool mine = (wave < 2) ? actor : critic;
+  const Net net = (wave < 2) ? ACTOR : CRITIC;
+  const int u0 = (wave & 1) * 32;   // first unit of this wave within its net
+  const int hrow = (wave >> 1) * H;  // actor rows 0..63, critic rows 64..127
+  if (mine) {
+    const float* W1 = L.w + net.w1;
+    const float* b1 = L.w + net.b1;
+#pragma unroll 2
+    for (int u = u0; u < u0 + 32; u++) {
+      float acc = 0.0f;
 #pragma unroll
-    for (int k = 0; k < NOBS; k++) A.obs_rows[(size_t)e * NOBS + k] = x[k];
+      for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
+      L.h1[(hrow + u) * PT_ENVS + lane] = tanhf(acc + b1[u]);
+    }
   }
-  const float* p = A.params;
-  float h[H];
-  if (A.value) {
-    trunk(p, CRITIC, x, c1, c2, 64, h);
-    A.value[e] = critic_head(p, h);
+  __syncthreads();
+  if (mine) {
+    float h[H];
+#pragma unroll
+    for (int k = 0; k < H; k++) h[k] = L.h1[(hrow + k) * PT_ENVS + lane];
+    const float* W2 = L.w + net.w2;
+    const float* b2 = L.w + net.b2;
+#pragma unroll 2
+    for (int u = u0; u < u0 + 32; u++) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
+      L.h2[(hrow + u) * PT_ENVS + lane] = tanhf(acc + b2[u]);
+    }
   }
-  trunk(p, ACTOR, x, c1, c2, 64, h);
+  __syncthreads();
+}
+
+__device__ __forceinline__ float tile_value(const PolicyLds& L, int lane) {
+  float v = 0.0f;
+#pragma unroll 8
+  for (int j = 0; j < H; j++) v = fmaf(L.w[ACKPPO_OFF_VAL_W + j], L.h2[(H + j) * PT_ENVS + lane], v);
+  return v + L.w[ACKPPO_OFF_VAL_B];
+}
+
+__device__ __forceinline__ void tile_mu(const PolicyLds& L, int lane, float mu[NA]) {
+#pragma unroll
+  for (int d = 0; d < NA; d++) {
+    float m = 0.0f;
+#pragma unroll 8
+    for (int j = 0; j < H; j++) m = fmaf(L.w[ACKPPO_OFF_ACT_W + d * H + j], L.h2[j * PT_ENVS + lane], m);
+    mu[d] = m + L.w[ACKPPO_OFF_ACT_B + d];
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_act_kernel(ActArgs A) {
+  extern __shared__ float lds_raw[];
+  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int e = blockIdx.x * PT_ENVS + lane;
+  const bool valid = e < A.n;
+  const int ec = valid ? e : A.n - 1;  // padding lanes recompute the last env, write nothing
+  stage_params(A.params, L.w);
+  float x[NOBS];
+  load_obs_soa(A.obs, A.n, ec, x);
+  __syncthreads();
+  if (A.obs_rows && valid && wave >= 2) {  // waves 2/3 copy the observation row (half each)
+    const int k0 = wave == 2 ? 0 : 40, k1 = wave == 2 ? 40 : NOBS;
+#pragma unroll
+    for (int k = 0; k < NOBS; k++)
+      if (k >= k0 && k < k1) A.obs_rows[(size_t)e * NOBS + k] = x[k];
+  }
+  policy_trunks(L, x, lane, wave, true, A.value != nullptr);
+  if (!valid) return;
+  if (wave == 2 && A.value) A.value[e] = tile_value(L, lane);
+  if (wave != 0) return;
+  const float* p = L.w;
   float mu[NA], a[NA];
-  actor_head(p, h, mu);
+  tile_mu(L, lane, mu);
   if (A.deterministic) {
     a[0] = mu[0];
     a[1] = mu[1];
@@ -180,34 +257,51 @@ extern "C" __global__ void __launch_bounds__(64) ackppo_act_kernel(ActArgs A) {
   if (A.log_prob) A.log_prob[e] = gauss_logp(a, mu, p);
 }
 
-extern "C" __global__ void __launch_bounds__(64) ackppo_value_kernel(const float* params, const float* obs, int n,
-                                                                     float* value) {
-  __shared__ float cols[2 * H * 64];
-  const int lane = threadIdx.x, e = blockIdx.x * 64 + lane;
-  if (e >= n) return;
-  float x[NOBS], h[H];
-  load_obs_soa(obs, n, e, x);
-  trunk(params, CRITIC, x, cols + lane, cols + H * 64 + lane, 64, h);
-  value[e] = critic_head(params, h);
+extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_value_kernel(const float* params, const float* obs,
+                                                                             int n, float* value) {
+  extern __shared__ float lds_raw[];
+  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int e = blockIdx.x * PT_ENVS + lane;
+  const int ec = e < n ? e : n - 1;
+  stage_params(params, L.w);
+  float x[NOBS];
+  load_obs_soa(obs, n, ec, x);
+  __syncthreads();
+  policy_trunks(L, x, lane, wave, false, true);
+  if (e < n && wave == 2) value[e] = tile_value(L, lane);
 }
 
-extern "C" __global__ void __launch_bounds__(64) ackppo_bootstrap_kernel(const float* params, const float* tobs,
-                                                                         const float* reward, const uint8_t* term,
-                                                                         const uint8_t* trunc, int n, float gamma,
-                                                                         float* reward_out, float* done_out) {
-  __shared__ float cols[2 * H * 64];
-  const int lane = threadIdx.x, e = blockIdx.x * 64 + lane;
-  if (e >= n) return;
-  float r = reward[e];
-  const bool te = term[e] != 0, tr = trunc[e] != 0;
-  if (tr && !te) {  // TimeLimit.truncated = truncated and not terminated (SB3 DummyVecEnv)
-    float x[NOBS], h[H];
-    load_obs_soa(tobs, n, e, x);
-    trunk(params, CRITIC, x, cols + lane, cols + H * 64 + lane, 64, h);
-    r += gamma * critic_head(params, h);
+// bootstrap: only tiles holding a truncated (not terminated) env run the critic
+extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_bootstrap_kernel(const float* params, const float* tobs,
+                                                                                 const float* reward,
+                                                                                 const uint8_t* term,
+                                                                                 const uint8_t* trunc, int n,
+                                                                                 float gamma, float* reward_out,
+                                                                                 float* done_out) {
+  extern __shared__ float lds_raw[];
+  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int e = blockIdx.x * PT_ENVS + lane;
+  const bool valid = e < n;
+  const int ec = valid ? e : n - 1;
+  const bool te = term[ec] != 0, tr = trunc[ec] != 0;
+  const bool boot = valid && tr && !te;  // TimeLimit.truncated = truncated and not terminated
+  if (__syncthreads_or(boot)) {
+    stage_params(params, L.w);
+    float x[NOBS];
+    load_obs_soa(tobs, n, ec, x);
+    __syncthreads();
+    policy_trunks(L, x, lane, wave, false, true);
   }
-  reward_out[e] = r;
-  done_out[e] = (te || tr) ? 1.0f : 0.0f;
+  if (valid && wave == 2) {
+    float r = reward[e];
+    if (boot) r += gamma * tile_value(L, lane);
+    reward_out[e] = r;
+    done_out[e] = (te || tr) ? 1.0f : 0.0f;
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(256) ackppo_gae_kernel(const float* rew, const float* val,
@@ -241,6 +335,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adv_stats_kernel(const 
     return;
   }
   double s = 0.0;
+#pragma unroll 8
   for (int i = lo + tid; i < hi; i += 256) s += adv[idx[i]];
   red[tid] = s;
   __syncthreads();
@@ -251,6 +346,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adv_stats_kernel(const 
   const double mean = red[0] / cnt;
   __syncthreads();
   double q = 0.0;
+#pragma unroll 8
   for (int i = lo + tid; i < hi; i += 256) {
     const double d = adv[idx[i]] - mean;
     q += d * d;
@@ -293,6 +389,7 @@ constexpr int T_VEC = T_NET + 2 * NET_SZ;
 constexpr int T_GMU = T_VEC, T_GLOG = T_VEC + 2 * LDP, T_GV = T_VEC + 4 * LDP;
 constexpr int T_TOTAL = T_VEC + 5 * LDP;
 static_assert(T_TOTAL * 4 <= 160 * 1024, "grad tile exceeds the 160 KiB LDS of a CU");
+constexpr int GRAD_THREADS = 256;
 
 // sum over the tile's samples of a[ra][s] * b[rb][s] for a 4x4 block of rows (16-B LDS reads)
 __device__ __forceinline__ void outer4x4(const float* a, const float* b, float acc[4][4]) {
@@ -343,7 +440,7 @@ __device__ __forceinline__ float row_dot(const float* a, const float* b) {
   return s;
 }
 
-extern "C" __global__ void __launch_bounds__(128) ackppo_grad_kernel(GradArgs A) {
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(GradArgs A) {
   extern __shared__ float tl[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar weight loads below
@@ -352,34 +449,62 @@ extern "C" __global__ void __launch_bounds__(128) ackppo_grad_kernel(GradArgs A)
   const int nvalid = min(TILE, A.batch - s0);
   const float* __restrict__ p = A.params;
 
-  // cooperative gather of the tile's observation rows into X [k][s] (zero rows for padding)
-  for (int i = tid; i < TILE * 80; i += 128) {
-    const int s = i / 80, k = i - s * 80;
-    float v = 0.0f;
-    if (s < nvalid && k < NOBS) v = A.obs_rows[(size_t)A.idx[s0 + s] * NOBS + k];
-    tl[T_X + k * LDP + s] = v;
+  // cooperative gather of the tile's observation rows into X [k][s] (zero rows for padding):
+  // thread t copies a quarter row (20 words) with all its loads in flight at once
+  {
+    const int s = tid >> 2, q = tid & 3;
+    const bool ok = s < nvalid;
+    const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + s] : 0) * NOBS;
+    float v[20];
+#pragma unroll
+    for (int i = 0; i < 20; i++) {
+      const int k = q * 20 + i;
+      v[i] = (ok && k < NOBS) ? row[k] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 20; i++) tl[T_X + (q * 20 + i) * LDP + s] = v[i];
   }
   __syncthreads();
 
-  // ---- per-sample forward / loss gradient / backward (wave 0 actor, wave 1 critic)
+  // ---- per-sample forward / loss gradient / backward. lane = sample; wave w works on net
+  // (w >> 1) (0 actor, 1 critic) and on units [32 (w & 1), +32) of each of its layers.
   const bool valid = lane < nvalid;
   const int sidx = valid ? A.idx[s0 + lane] : 0;
-  const Net net = wave == 0 ? ACTOR : CRITIC;
-  float* nt = tl + T_NET + wave * NET_SZ;
-  float* c1 = nt + T_H1 + lane;
-  float* c2 = nt + T_H2 + lane;
-  float* cd2 = nt + T_D2 + lane;
-  float* cd1 = nt + T_D1 + lane;
+  const int nid = wave >> 1, u0 = (wave & 1) * 32;
+  const Net net = nid == 0 ? ACTOR : CRITIC;
+  float* nt = tl + T_NET + nid * NET_SZ;
   const float invB = 1.0f / (float)A.batch;
-  float h[H];
-  {
+  {  // layer 1
     float x[NOBS];
     load_col(tl + T_X + lane, LDP, x);
-    trunk(p, net, x, c1, c2, LDP, h);
+    const float* W1 = p + net.w1;
+#pragma unroll 2
+    for (int u = u0; u < u0 + 32; u++) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
+      nt[T_H1 + u * LDP + lane] = tanhf(acc + p[net.b1 + u]);
+    }
   }
+  __syncthreads();
+  {  // layer 2
+    float h[H];
+    load_col(nt + T_H1 + lane, LDP, h);
+    const float* W2 = p + net.w2;
+#pragma unroll 2
+    for (int u = u0; u < u0 + 32; u++) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
+      nt[T_H2 + u * LDP + lane] = tanhf(acc + p[net.b2 + u]);
+    }
+  }
+  __syncthreads();
+  // heads and the loss gradient w.r.t. their outputs (waves 0 and 2)
   float loss_a = 0.0f, loss_b = 0.0f, loss_c = 0.0f;
   if (wave == 0) {
-    float mu[NA], a[NA];
+    float h[H], mu[NA], a[NA];
+    load_col(nt + T_H2 + lane, LDP, h);
     actor_head(p, h, mu);
     a[0] = A.actions[2 * (size_t)sidx];
     a[1] = A.actions[2 * (size_t)sidx + 1];
@@ -392,72 +517,85 @@ extern "C" __global__ void __launch_bounds__(128) ackppo_grad_kernel(GradArgs A)
     // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
     // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
     const float glogp = valid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
-    float gmu[NA];
 #pragma unroll
     for (int d = 0; d < NA; d++) {
       const float sigma = expf(p[ACKPPO_OFF_LOG_STD + d]);
       const float dv = a[d] - mu[d];
-      gmu[d] = glogp * dv / (sigma * sigma);
-      tl[T_GMU + d * LDP + lane] = gmu[d];
+      tl[T_GMU + d * LDP + lane] = glogp * dv / (sigma * sigma);
       tl[T_GLOG + d * LDP + lane] = glogp * (dv * dv / (sigma * sigma) - 1.0f);
     }
-#pragma unroll
-    for (int j = 0; j < H; j++)
-      cd2[j * LDP] = (gmu[0] * p[ACKPPO_OFF_ACT_W + j] + gmu[1] * p[ACKPPO_OFF_ACT_W + H + j]) * (1.0f - h[j] * h[j]);
     if (valid) {
       loss_a = -fminf(l1, l2);
       loss_b = (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
       loss_c = (r - 1.0f) - lr;
     }
-  } else {
+  } else if (wave == 2) {
+    float h[H];
+    load_col(nt + T_H2 + lane, LDP, h);
     const float v = critic_head(p, h);
     const float R = A.ret[sidx];
-    const float gv = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
-    tl[T_GV + lane] = gv;
-#pragma unroll
-    for (int j = 0; j < H; j++) cd2[j * LDP] = gv * p[ACKPPO_OFF_VAL_W + j] * (1.0f - h[j] * h[j]);
+    tl[T_GV + lane] = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
     if (valid) loss_a = (R - v) * (R - v);
   }
-  // d1[k] = (sum_j d2[j] W2[j][k]) (1 - h1[k]^2)
-  {
-    float d1[H];
-#pragma unroll
-    for (int k = 0; k < H; k++) d1[k] = 0.0f;
-    const float* W2 = p + net.w2;
-#pragma unroll 2
-    for (int j = 0; j < H; j++) {
-      const float dj = cd2[j * LDP];
-#pragma unroll
-      for (int k = 0; k < H; k++) d1[k] = fmaf(dj, W2[j * H + k], d1[k]);
+  __syncthreads();
+  // d2[u] = (dL/dh2[u]) (1 - h2[u]^2) for this wave's units
+  if (nid == 0) {
+    const float g0 = tl[T_GMU + lane], g1 = tl[T_GMU + LDP + lane];
+#pragma unroll 4
+    for (int u = u0; u < u0 + 32; u++) {
+      const float hu = nt[T_H2 + u * LDP + lane];
+      nt[T_D2 + u * LDP + lane] = (g0 * p[ACKPPO_OFF_ACT_W + u] + g1 * p[ACKPPO_OFF_ACT_W + H + u]) * (1.0f - hu * hu);
     }
-#pragma unroll
-    for (int k = 0; k < H; k++) {
-      const float hk = c1[k * LDP];
-      cd1[k * LDP] = d1[k] * (1.0f - hk * hk);
+  } else {
+    const float gv = tl[T_GV + lane];
+#pragma unroll 4
+    for (int u = u0; u < u0 + 32; u++) {
+      const float hu = nt[T_H2 + u * LDP + lane];
+      nt[T_D2 + u * LDP + lane] = gv * p[ACKPPO_OFF_VAL_W + u] * (1.0f - hu * hu);
     }
   }
-  // loss statistics of the tile
-  loss_a = wave_sum(loss_a);
-  loss_b = wave_sum(loss_b);
-  loss_c = wave_sum(loss_c);
-  if (lane == 0) {
-    float* lp = A.lpart + (size_t)blk * ACKPPO_NLOSS;
-    if (wave == 0) {
-      lp[0] = loss_a;
-      lp[2] = loss_b;
-      lp[3] = loss_c;
-      lp[4] = (float)nvalid;
-      lp[5] = lp[6] = lp[7] = 0.0f;
-    } else {
-      lp[1] = loss_a;
+  __syncthreads();
+  {  // d1[k] = (sum_j d2[j] W2[j][k]) (1 - h1[k]^2) for this wave's k in [u0, u0+32)
+    float d1[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) d1[k] = 0.0f;
+    const float* W2 = p + net.w2 + u0;
+#pragma unroll 2
+    for (int j = 0; j < H; j++) {
+      const float dj = nt[T_D2 + j * LDP + lane];
+#pragma unroll
+      for (int k = 0; k < 32; k++) d1[k] = fmaf(dj, W2[j * H + k], d1[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      const float hk = nt[T_H1 + (u0 + k) * LDP + lane];
+      nt[T_D1 + (u0 + k) * LDP + lane] = d1[k] * (1.0f - hk * hk);
+    }
+  }
+  // loss statistics of the tile (waves 0 and 2 hold them)
+  if (wave == 0 || wave == 2) {
+    loss_a = wave_sum(loss_a);
+    loss_b = wave_sum(loss_b);
+    loss_c = wave_sum(loss_c);
+    if (lane == 0) {
+      float* lp = A.lpart + (size_t)blk * ACKPPO_NLOSS;
+      if (wave == 0) {
+        lp[0] = loss_a;
+        lp[2] = loss_b;
+        lp[3] = loss_c;
+        lp[4] = (float)nvalid;
+        lp[5] = lp[6] = lp[7] = 0.0f;
+      } else {
+        lp[1] = loss_a;
+      }
     }
   }
   __syncthreads();
 
-  // ---- weight gradients: sums over the tile of outer products (both waves, all nets)
+  // ---- weight gradients: sums over the tile of outer products (all waves, both nets)
   float* g = A.gpart + (size_t)blk * P;
   // layer 1: [64 units][79 inputs] per net as 4x4 blocks (16 x 20 blocks per net)
-  for (int b = tid; b < 2 * 16 * 20; b += 128) {
+  for (int b = tid; b < 2 * 16 * 20; b += GRAD_THREADS) {
     const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
     const float* net_t = tl + T_NET + nn * NET_SZ;
     float acc[4][4];
@@ -470,7 +608,7 @@ extern "C" __global__ void __launch_bounds__(128) ackppo_grad_kernel(GradArgs A)
         if (4 * kb + j < NOBS) g[w1 + (4 * jb + i) * NOBS + 4 * kb + j] = acc[i][j];
   }
   // layer 2: [64][64] per net (16 x 16 blocks per net)
-  for (int b = tid; b < 2 * 16 * 16; b += 128) {
+  for (int b = tid; b < 2 * 16 * 16; b += GRAD_THREADS) {
     const int nn = b / 256, r = b - nn * 256, jb = r / 16, kb = r - jb * 16;
     const float* net_t = tl + T_NET + nn * NET_SZ;
     float acc[4][4];
@@ -484,7 +622,7 @@ extern "C" __global__ void __launch_bounds__(128) ackppo_grad_kernel(GradArgs A)
   // biases, heads, log_std
   const float* an = tl + T_NET;
   const float* cn = tl + T_NET + NET_SZ;
-  for (int i = tid; i < 453; i += 128) {
+  for (int i = tid; i < 453; i += GRAD_THREADS) {
     if (i < 64) g[ACKPPO_OFF_PI_B1 + i] = row_sum(an + T_D1 + i * LDP);
     else if (i < 128) g[ACKPPO_OFF_PI_B2 + i - 64] = row_sum(an + T_D2 + (i - 64) * LDP);
     else if (i < 192) g[ACKPPO_OFF_VF_B1 + i - 128] = row_sum(cn + T_D1 + (i - 128) * LDP);
@@ -503,8 +641,15 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
                                                                        float ent_coef, float* grad, float* loss) {
   const int pidx = blockIdx.x * 256 + threadIdx.x;
   if (pidx < P) {
-    float s = 0.0f;
-    for (int b = 0; b < nblk; b++) s += gpart[(size_t)b * P + pidx];
+    // 8 independent partial sums keep 8 row loads in flight per thread
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = 0;
+    for (; b + 8 <= nblk; b += 8) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc[i] += gpart[(size_t)(b + i) * P + pidx];
+    }
+    for (; b < nblk; b++) acc[0] += gpart[(size_t)b * P + pidx];
+    float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
     grad[pidx] = s;
   }
@@ -523,6 +668,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* para
   const int tid = threadIdx.x;
   // every block forms the global norm itself (75 KB from L2) instead of a second launch
   float ss = 0.0f;
+#pragma unroll 8
   for (int i = tid; i < P; i += 256) {
     const float gi = grad[i] * scale;
     ss = fmaf(gi, gi, ss);
@@ -564,6 +710,17 @@ int launched(const char* what) {
 }
 constexpr size_t GRAD_LDS = (size_t)T_TOTAL * sizeof(float);
 bool g_grad_attr = false;
+bool g_policy_attr = false;
+bool policy_lds_ready() {
+  if (g_policy_attr) return true;
+  const void* ks[3] = {(const void*)ackppo_act_kernel, (const void*)ackppo_value_kernel,
+                       (const void*)ackppo_bootstrap_kernel};
+  for (const void* k : ks)
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(PolicyLds)) != hipSuccess)
+      return false;
+  g_policy_attr = true;
+  return true;
+}
 }  // namespace
 
 extern "C" {
@@ -576,15 +733,18 @@ int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env
   if (!params || !obs_soa || !env_action || n_env < 0) return fail(ACKPPO_EINVAL, "ackppo_act: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
   ActArgs A{params, obs_soa, n_env, env_offset, seed, step, deterministic, obs_rows, action, env_action, log_prob, value};
-  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + 63) / 64), dim3(64), 0, (hipStream_t)stream, A);
+  if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_act: cannot reserve the policy LDS tile");
+  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS), sizeof(PolicyLds),
+                     (hipStream_t)stream, A);
   return launched("ackppo_act");
 }
 
 int ackppo_value(const float* params, const float* obs_soa, int n_env, float* value, void* stream) {
   if (!params || !obs_soa || !value || n_env < 0) return fail(ACKPPO_EINVAL, "ackppo_value: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
-  hipLaunchKernelGGL(ackppo_value_kernel, dim3((n_env + 63) / 64), dim3(64), 0, (hipStream_t)stream, params, obs_soa,
-                     n_env, value);
+  if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_value: cannot reserve the policy LDS tile");
+  hipLaunchKernelGGL(ackppo_value_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS), sizeof(PolicyLds),
+                     (hipStream_t)stream, params, obs_soa, n_env, value);
   return launched("ackppo_value");
 }
 
@@ -593,8 +753,10 @@ int ackppo_bootstrap(const float* params, const float* terminal_obs_soa, const f
   if (!params || !terminal_obs_soa || !reward || !term || !trunc || !reward_out || !done_out || n_env < 0)
     return fail(ACKPPO_EINVAL, "ackppo_bootstrap: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
-  hipLaunchKernelGGL(ackppo_bootstrap_kernel, dim3((n_env + 63) / 64), dim3(64), 0, (hipStream_t)stream, params,
-                     terminal_obs_soa, reward, term, trunc, n_env, gamma, reward_out, done_out);
+  if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_bootstrap: cannot reserve the policy LDS tile");
+  hipLaunchKernelGGL(ackppo_bootstrap_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS),
+                     sizeof(PolicyLds), (hipStream_t)stream, params, terminal_obs_soa, reward, term, trunc, n_env,
+                     gamma, reward_out, done_out);
   return launched("ackppo_bootstrap");
 }
 
@@ -635,7 +797,8 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
   }
   GradArgs A{params, obs_rows, actions, old_log_prob, advantages, returns, idx, batch, stats, clip_range, ent_coef,
              vf_coef, grad_partial, loss_partial};
-  hipLaunchKernelGGL(ackppo_grad_kernel, dim3((batch + TILE - 1) / TILE), dim3(128), GRAD_LDS, (hipStream_t)stream, A);
+  hipLaunchKernelGGL(ackppo_grad_kernel, dim3((batch + TILE - 1) / TILE), dim3(GRAD_THREADS), GRAD_LDS,
+                     (hipStream_t)stream, A);
   return launched("ackppo_grad");
 }
 
