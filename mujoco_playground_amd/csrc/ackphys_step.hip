@@ -33,7 +33,33 @@ __device__ unsigned long long* g_stamps;
     __builtin_amdgcn_sched_barrier(0);                                                    \
     if ((threadIdx.x & 63) == 0) g_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;       \
   } while (0)
+// Newton-phase accumulators (diag build): NT_MARK(ph) adds the cycles since the previous mark to phase ph
+#define NT_DECL unsigned long long _nt_acc[5] = {0, 0, 0, 0, 0}, _nt_last = 0;
+#define NT_NOW(v)                                                                \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");     \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+  } while (0)
+#define NT_START NT_NOW(_nt_last)
+#define NT_MARK(ph)                 \
+  do {                              \
+    unsigned long long _t;          \
+    NT_NOW(_t);                     \
+    _nt_acc[ph] += _t - _nt_last;   \
+    _nt_last = _t;                  \
+  } while (0)
+#define NT_FLUSH                                                                                              \
+  do {                                                                                                        \
+    if ((threadIdx.x & 63) == 0)                                                                              \
+      for (int _p = 0; _p < 5; _p++)                                                                          \
+        g_stamps[(16 + 64 + _p) * (size_t)gridDim.x + blockIdx.x] = _nt_acc[_p];                              \
+  } while (0)
 #else
+#define NT_DECL
+#define NT_START
+#define NT_MARK(ph)
+#define NT_FLUSH
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -179,18 +205,21 @@ __device__ __forceinline__ ObsOut observe_head(const float p[3], const float q[4
   return o;
 }
 
-__device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
-  // site origin / direction (chassis frame) -> world; mj_ray plane test (ray_plane)
-  const float ox = RAY_ORG[i][0], oy = RAY_ORG[i][1], dxb = RAY_DIR[i][0], dyb = RAY_DIR[i][1];
+// site origin (ox, oy, RAY_Z) / direction (dxb, dyb, 0) in the chassis frame -> world; mj_ray
+// plane test (ray_plane) against the finite floor rectangle
+__device__ __forceinline__ float ray_floor_c(const float p[3], const float R[9], float ox, float oy, float dxb,
+                                             float dyb) {
   float dz = R[6] * dxb + R[7] * dyb;
   float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
-  if (dz > -MINVAL) return -1.0f;
-  float t = -oz / dz;
-  if (t < 0) return -1.0f;
-  float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
-  float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
-  if (fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1]) return fminf(t, RAY_CUTOFF);
-  return -1.0f;
+  // branchless: t from the hardware reciprocal (<= 2 ulp; f32 tolerance of the obs parity)
+  const float t = __fdividef(-oz, dz);
+  const float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
+  const float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
+  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
+  return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
+}
+__device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
+  return ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
 }
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
@@ -201,7 +230,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
-#pragma unroll 8
+#pragma unroll
   for (int i = 10; i < 72; i++) {
     float v = ray_floor(p, R, i);
     dst[(size_t)i * n] = v;
@@ -509,6 +538,46 @@ __device__ __forceinline__ void ls_row(float x, float jp, float D, int type, flo
     else if (x >= Rfl) g += fl * jp;
     else { g += D * x * jp; h += D * jp * jp; }
   } else if (x < 0.0f) { g += D * x * jp; h += D * jp * jp; }
+}
+
+// pairwise sum (independent adds: ILP for a lone wave, whose dependent VALU chain issues every 4+ cycles)
+template <int N>
+__device__ __forceinline__ float tsum(const float (&v)[N]) {
+  float t[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = v[i];
+#pragma unroll
+  for (int w = 1; w < N; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < N; i += 2 * w) t[i] += t[i + w];
+  return t[0];
+}
+
+// line-search derivative phi'(al) / phi''(al) contributions of the scalar rows (equality,
+// frictionloss Huber, limits), branchless; only rows with (r & MASK) == sel (the quad kernel
+// splits them over its 4 lanes)
+template <int MASK>
+__device__ __forceinline__ void scal_ls(float al, const float sj[NSCAL], const float sjp[NSCAL], const float sD[NSCAL],
+                                        const float sRfl[NSCAL], const float sfl[NSCAL], const bool sact[NSCAL], int sel,
+                                        float& g, float& h) {
+  float gs[NSCAL], hs[NSCAL];
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++) {
+    const float jp = sjp[r], x = fmaf(al, jp, sj[r]);
+    bool quad;
+    float lin = 0.0f;
+    if (r == 0) quad = true;
+    else if (r <= 6) {
+      quad = x > -sRfl[r] && x < sRfl[r];
+      lin = x <= -sRfl[r] ? -sfl[r] : sfl[r];
+    } else quad = x < 0.0f;
+    const bool on = sact[r] && ((r & MASK) == sel);
+    const float Djp = sD[r] * jp;
+    gs[r] = on ? (quad ? Djp * x : lin * jp) : 0.0f;
+    hs[r] = (on && quad) ? Djp * jp : 0.0f;
+  }
+  g += tsum(gs);
+  h += tsum(hs);
 }
 
 template <int CH>
@@ -990,6 +1059,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   // region boundary), or after MAXIT iterations.
   bool exact = false;
   int it_done = MAXIT, why = 4;
+  NT_DECL
+  NT_START;
 #pragma unroll 1
   for (int it = 0; it < MAXIT; it++) {
     if (exact) { it_done = it; if (why != 2) why = 1; break; }
@@ -1036,11 +1107,13 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     }
     FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad);
     (void)gscale;
+    NT_MARK(0);
     chol12(H);
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
     chol12_solve(H, pdir);
+    NT_MARK(1);
     // Jp for all rows
     FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir);
 #pragma unroll
@@ -1052,14 +1125,9 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 #pragma unroll
     for (int i = 0; i < NV; i++) { pMp += pdir[i] * Mp[i]; pg0 += Mp[i] * (a[i] - sv.a0[i]); }
     auto dphi = [&](float al, float& g, float& h) __attribute__((always_inline)) {
-      g = pg0 + al * pMp;
+      g = fmaf(al, pMp, pg0);
       h = pMp;
-#pragma unroll
-      for (int r = 0; r < NSCAL; r++) {
-        if (!sact[r]) continue;
-        int type = r == 0 ? 0 : (r <= 6 ? 1 : 2);
-        ls_row(sj[r] + al * sjp[r], sjp[r], sD[r], type, sRfl[r], sfl[r], g, h);
-      }
+      scal_ls<0>(al, sj, sjp, sD, sRfl, sfl, sact, 0, g, h);
       FOR_SLOTS(S, S.wmask, s) {
         float D = S.at(s, 3);
 #pragma unroll
@@ -1075,6 +1143,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 #pragma unroll
     for (int i = 0; i < NV; i++) g0 += grad[i] * pdir[i];
     if (!(g0 < 0.0f)) { it_done = it; why = 3; break; }  // no descent left: optimum to f32 precision
+    NT_MARK(2);
     float lo = 0.0f, hi = 3.0e38f, al = 1.0f;
     bool full = false;
 #pragma unroll 1
@@ -1089,6 +1158,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       al = nal;
       if (tiny) break;
     }
+    NT_MARK(3);
     // move, count row-state changes; "still" = the update is below f32 resolution of a
     int changed = 0;
     bool still = true;
@@ -1117,8 +1187,10 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     }
     exact = (full && changed == 0) || still;
     if (still && !(full && changed == 0)) why = 2;
+    NT_MARK(4);
   }
   STAMP(6);
+  NT_FLUSH;
 #ifdef AK_STAMPS
   g_stamps[16 * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] = (unsigned long long)(it_done * 8 + why);
 #else

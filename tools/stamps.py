@@ -32,13 +32,15 @@ def main():
     dev = torch.device("cuda:0")
     ctx = P()
     assert L.ackphys_create(blob, len(blob), n, 0, C.byref(ctx)) == 0
+    L.ackphys_set_variant.argtypes = [P, C.c_int]
+    assert L.ackphys_set_variant(ctx, 0) == 0  # stamps are in the lane-per-env kernel
     state = torch.zeros(44, n, device=dev)
     obs = torch.zeros(79, n, device=dev)
     rew = torch.zeros(n, device=dev)
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
     nb = (n + 63) // 64
-    stamps = torch.zeros(16 * nb + nb * 64, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(16 * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
     p = lambda t: P(t.data_ptr())
     stream = P(torch.cuda.current_stream().cuda_stream)
@@ -60,7 +62,12 @@ def main():
             allv = stamps.cpu().numpy()
             s = allv[: 16 * nb].reshape(16, nb)[:11]
             res.append(np.diff(s, axis=0))
-            its = allv[16 * nb:]
+            its = allv[16 * nb:16 * nb + 64 * nb]
+            nt = allv[16 * nb + 64 * nb:].reshape(5, nb)
+            if k == 200:
+                print("  newton phases (median cycles/wave, summed over iterations): " + ", ".join(
+                    f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"])))
+            its = its[: 64 * nb]
             if k == 200:
                 itn, why = its // 8, its % 8
                 wmax = itn.reshape(nb, 64).max(axis=1)
