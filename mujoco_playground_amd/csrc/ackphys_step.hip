@@ -263,8 +263,7 @@ __device__ __forceinline__ float ray_floor_c(const float p[3], const float R[9],
   const float t = -oz * __builtin_amdgcn_rcpf(dz);
   const float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
   const float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
-  // bitwise & (no short-circuit): no branch per ray
-  const bool hit = (dz <= -MINVAL) & (t >= 0.0f) & (fabsf(hx) <= FLOOR_SIZE[0]) & (fabsf(hy) <= FLOOR_SIZE[1]);
+  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
   return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
 }
 __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
