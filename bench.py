@@ -197,17 +197,16 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
     return parity, base
 
 
-def load_traffic(contacts: bool, kern_name="ackphys_step_kernel"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/profile_pmc.py);
-    None if that profile is absent or was taken on another workload."""
+def load_pmc(kern_name: str, contacts: bool):
+    """PMC summary of the kernel from the committed rocprofv3 passes (tools/profile_pmc.py); None if
+    that profile is absent or was taken on another workload."""
     path = os.path.join(HERE, "profiles", "pmc_latest.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        k = d.get(kern_name, {})
-        if bool(k.get("contacts")) != contacts:
+            k = json.load(f).get(kern_name)
+        if not k or bool(k.get("contacts")) != contacts:
             return None
-        return k.get("hbm_bytes_per_launch")
+        return k
     except (OSError, ValueError):
         return None
 
@@ -243,7 +242,17 @@ def main():
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
     bpe = algorithmic_bytes_per_env_step()
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(contacts)
+    kern = "ackphys_step_quad_kernel" if (a.variant == "quad" or (a.variant == "auto" and contacts)) \
+        else "ackphys_step_kernel"
+    pmc = load_pmc(kern, contacts)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    valu = None
+    if pmc and pmc.get("valu_insts_per_wave"):
+        # one wave alone issues a VALU op every 4 cycles (MI355X_MICROARCH.md constants table)
+        valu = {"insts_per_wave": pmc["valu_insts_per_wave"], "waves": pmc["SQ_WAVES"],
+                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave"] * 4 / (kern_ms * 1e-3 * 2.4e9),
+                "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave rate "
+                        "(4 cyc/op, 2.4 GHz); the rest is dependency/memory latency"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -256,9 +265,7 @@ def main():
                        "parallelism": f"dp{world} (independent env shards, 1 all_gather of episode stats)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ackphys_step_quad_kernel" if (a.variant == "quad" or (a.variant == "auto" and contacts))
-                         else "ackphys_step_kernel",
-                         "kernel_ms": kern_ms,
+                         "kernel": kern, "kernel_ms": kern_ms, "valu": valu,
                          "algorithmic_bytes_per_env_step": bpe,
                          "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,

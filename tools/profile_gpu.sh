@@ -8,6 +8,6 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o prof -- \
-  python3 $ROOT/bench.py --no-cpu --no-secondary --steps 300 --warmup 30 > $OUT/bench_stdout.json 2> $OUT/stderr.log
+  python3 $ROOT/bench.py --no-cpu --steps 300 --warmup 30 > $OUT/bench_stdout.json 2> $OUT/stderr.log
 find $OUT -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 cat $OUT/kernel_stats.csv | head -20

@@ -1,12 +1,14 @@
-"""rocprofv3 PMC passes for the step kernel -> profiles/pmc_latest.json (run on the GPU box).
+"""rocprofv3 PMC passes for the step kernels -> gpurun_out/pmc_latest.json (run on the GPU box).
 
-Separate passes (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950), kernel-trace
-only, no sys/runtime trace. Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B
-requests at 64 B for lane-contiguous streaming reads -> doubled; WRITE_SIZE taken as reported
-(dword-per-lane stores: uncalibrated, noted).
-    python3 tools/profile_pmc.py [--contacts 0]
+For each workload (contacts off -> ackphys_step_kernel, contacts on -> ackphys_step_quad_kernel,
+the kernels bench.py's AUTO mapping runs) three separate passes, kernel-trace only, no
+sys/runtime trace:
+  FETCH_SIZE, WRITE_SIZE (HBM bytes; they do not fit one TCC pass on gfx950),
+  SQ_INSTS_VALU + SQ_INSTS_SALU + SQ_WAVES (instruction mix, one SQ pass).
+Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B requests at 64 B for
+lane-contiguous streaming reads -> doubled; WRITE_SIZE taken as reported.
+    python3 tools/profile_pmc.py
 """
-import argparse
 import csv
 import glob
 import json
@@ -15,39 +17,39 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {0: "ackphys_step_kernel", 1: "ackphys_step_quad_kernel"}
 
 
-def run_pass(counter, out, contacts):
+def run_pass(counters, out, contacts):
     os.makedirs(out, exist_ok=True)
-    cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", out, "-o",
-           "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--steps", "60",
-           "--warmup", "5", "--contacts", str(contacts)]
+    cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
+           "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
+           "--steps", "60", "--warmup", "5", "--contacts", str(contacts)]
     env = dict(os.environ, TMPDIR="/tmp")
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, stdout=subprocess.DEVNULL)
-    vals = []
+    vals = {c: [] for c in counters}
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if row.get("Kernel_Name", "").startswith("ackphys_step_kernel") and row.get("Counter_Name") == counter:
-                vals.append(float(row["Counter_Value"]))
-    return vals
+            if row.get("Kernel_Name", "").startswith(KERNELS[contacts]) and row.get("Counter_Name") in vals:
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {c: (sorted(v)[len(v) // 2] if v else None) for c, v in vals.items()}  # median dispatch
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--contacts", type=int, default=0)
-    a = ap.parse_args()
-    out = os.path.join(ROOT, "gpurun_out", "pmc")
-    fetch = run_pass("FETCH_SIZE", out + "_fetch", a.contacts)
-    write = run_pass("WRITE_SIZE", out + "_write", a.contacts)
-    # steady state: drop the warmup dispatches
-    f = sorted(fetch)[len(fetch) // 2] if fetch else None
-    w = sorted(write)[len(write) // 2] if write else None
-    res = {"ackphys_step_kernel": {
-        "contacts": bool(a.contacts), "dispatches": [len(fetch), len(write)],
-        "FETCH_SIZE_kB_median": f, "WRITE_SIZE_kB_median": w,
-        "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if (f is not None and w is not None) else None,
-        "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
-        "algorithmic_bytes_per_launch": 690 * 4096}}
+    res = {}
+    for contacts, kern in KERNELS.items():
+        out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}")
+        f = run_pass(["FETCH_SIZE"], out + "_fetch", contacts)["FETCH_SIZE"]
+        w = run_pass(["WRITE_SIZE"], out + "_write", contacts)["WRITE_SIZE"]
+        sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts)
+        res[kern] = {
+            "contacts": bool(contacts), "FETCH_SIZE_kB_median": f, "WRITE_SIZE_kB_median": w,
+            "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if (f is not None and w is not None) else None,
+            "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
+            "algorithmic_bytes_per_launch": 690 * 4096,
+            "SQ_INSTS_VALU": sq["SQ_INSTS_VALU"], "SQ_INSTS_SALU": sq["SQ_INSTS_SALU"], "SQ_WAVES": sq["SQ_WAVES"],
+            "valu_insts_per_wave": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]) if sq["SQ_WAVES"] else None,
+        }
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
