@@ -1202,7 +1202,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       dphi(al, g, h);
       if (fabsf(g) <= 1e-4f * fabsf(g0)) { full = (k == 0); break; }
       if (g < 0.0f) lo = al; else hi = al;
-      float nal = al - g / h;
+      float nal = al - g * __builtin_amdgcn_rcpf(h);  // a proposal inside the bracket: 1-ulp rcp suffices
       if (!(nal > lo && nal < hi)) nal = (hi < 3.0e38f) ? 0.5f * (lo + hi) : 2.0f * al;
       bool tiny = fabsf(nal - al) <= 1e-6f * al;
       al = nal;
