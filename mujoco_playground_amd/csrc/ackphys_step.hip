@@ -630,6 +630,28 @@ __device__ __forceinline__ void scal_ls(float al, const float sj[NSCAL], const f
   h += tsum(hs);
 }
 
+// f32 noise scale of phi'(alpha) (sum of the magnitudes of its terms at alpha = 0): the line
+// search accepts |phi'| below 1e-6 of it -- at the optimum the Newton direction is rounding
+// noise and a purely relative test (1e-4 |phi'(0)|) can never be met
+template <int MASK>
+__device__ __forceinline__ float scal_noise(const float sj[NSCAL], const float sjp[NSCAL], const float sD[NSCAL],
+                                            const float sRfl[NSCAL], const float sfl[NSCAL], const bool sact[NSCAL],
+                                            int sel) {
+  float t[NSCAL];
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++) {
+    const float x = sj[r], jp = sjp[r];
+    bool quad;
+    if (r == 0) quad = true;
+    else if (r <= 6) quad = x > -sRfl[r] && x < sRfl[r];
+    else quad = x < 0.0f;
+    const bool on = sact[r] && ((r & MASK) == sel);
+    const bool lin = r >= 1 && r <= 6 && !quad;
+    t[r] = on ? (quad ? sD[r] * (fabsf(x * jp) + jp * jp) : (lin ? sfl[r] * fabsf(jp) : 0.0f)) : 0.0f;
+  }
+  return tsum(t);
+}
+
 template <int CH>
 __device__ __forceinline__ void slot_loop_hess(const Slots& S, const float dirs[3][3], const float sa[2][3],
                                                float H[NV][NV], float grad[NV]) {
@@ -1193,6 +1215,16 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 #pragma unroll
     for (int i = 0; i < NV; i++) g0 += grad[i] * pdir[i];
     if (!(g0 < 0.0f)) { it_done = it; why = 3; break; }  // no descent left: optimum to f32 precision
+    float ns = fabsf(pg0) + fabsf(pMp) + scal_noise<0>(sj, sjp, sD, sRfl, sfl, sact, 0);
+    FOR_SLOTS(S, S.wmask, s) {
+      const float D = S.at(s, 3);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const float x = S.at(s, 4 + r), jp = S.at(s, 8 + r);
+        if (x < 0.0f) ns += D * (fabsf(x * jp) + jp * jp);
+      }
+    }
+    const float gtol = fmaxf(1e-4f * fabsf(g0), 1e-6f * ns);
     NT_MARK(2);
     float lo = 0.0f, hi = 3.0e38f, al = 1.0f;
     bool full = false;
@@ -1200,7 +1232,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     for (int k = 0; k < LSIT; k++) {
       float g, h;
       dphi(al, g, h);
-      if (fabsf(g) <= 1e-4f * fabsf(g0)) { full = (k == 0); break; }
+      if (fabsf(g) <= gtol) { full = (k == 0); break; }
       if (g < 0.0f) lo = al; else hi = al;
       float nal = al - g * __builtin_amdgcn_rcpf(h);  // a proposal inside the bracket: 1-ulp rcp suffices
       if (!(nal > lo && nal < hi)) nal = (hi < 3.0e38f) ? 0.5f * (lo + hi) : 2.0f * al;
