@@ -631,7 +631,7 @@ __device__ __forceinline__ void scal_ls(float al, const float sj[NSCAL], const f
 }
 
 // f32 noise scale of phi'(alpha) (sum of the magnitudes of its terms at alpha = 0): the line
-// search accepts |phi'| below 1e-6 of it -- at the optimum the Newton direction is rounding
+// search accepts |phi'| below 1e-5 of it -- at the optimum the Newton direction is rounding
 // noise and a purely relative test (1e-4 |phi'(0)|) can never be met
 template <int MASK>
 __device__ __forceinline__ float scal_noise(const float sj[NSCAL], const float sjp[NSCAL], const float sD[NSCAL],
@@ -1224,7 +1224,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
         if (x < 0.0f) ns += D * (fabsf(x * jp) + jp * jp);
       }
     }
-    const float gtol = fmaxf(1e-4f * fabsf(g0), 1e-6f * ns);
+    const float gtol = fmaxf(1e-4f * fabsf(g0), 1e-5f * ns);
     NT_MARK(2);
     float lo = 0.0f, hi = 3.0e38f, al = 1.0f;
     bool full = false;
@@ -1269,6 +1269,12 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     }
     exact = (full && changed == 0) || still;
     if (still && !(full && changed == 0)) why = 2;
+#ifdef AK_TRACE
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+      printf("[trace] it %d al %.7g full %d changed %d still %d g0 %.6g gtol %.6g ns %.6g pMp %.6g pg0 %.6g |p|inf %.6g\n", it, al,
+             (int)full, changed, (int)still, g0, gtol, ns, pMp, pg0,
+             fmaxf(fmaxf(fabsf(pdir[6]), fabsf(pdir[8])), fmaxf(fabsf(pdir[0]), fabsf(pdir[3]))));
+#endif
     NT_MARK(4);
   }
   STAMP(6);
