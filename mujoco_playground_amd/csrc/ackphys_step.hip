@@ -135,20 +135,17 @@ __device__ __forceinline__ void stf_lane_row(const Soa& b, int k, uint32_t vo, f
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b.r, vo + (uint32_t)k * b.row, 0, 0);
 }
 
-// observation destination: always `a` (the obs buffer), plus `b` (terminal obs) on lanes that
-// auto-reset -- their `a` words are overwritten by the reset observation afterwards. Both
-// descriptors stay wave-uniform (a lane-selected descriptor is waterfalled on every store).
-struct ObsDst {
-  Soa a, b;
-  bool use_b;
-};
-__device__ __forceinline__ void stf(const ObsDst& d, int k, uint32_t vo, float v) {
-  stf(d.a, k, vo, v);
-  if (d.use_b) stf(d.b, k, vo, v);
-}
-__device__ __forceinline__ void stf_lane_row(const ObsDst& d, int k, uint32_t vo, float v) {
-  stf_lane_row(d.a, k, vo, v);
-  if (d.use_b) stf_lane_row(d.b, k, vo, v);
+// terminal observation of auto-resetting lanes: copy the 79 words this lane just wrote to `obs`
+// into `tobs` (before the reset overwrites them). The common step never enters this (wave-uniform
+// test), so the observation stores stay single, unconditional and uniform-descriptor.
+__device__ __forceinline__ void copy_terminal_obs(const Soa& obs, const Soa& tobs, uint32_t vo, bool mine) {
+  if (__builtin_amdgcn_ballot_w64(mine) == 0ull) return;
+  __builtin_amdgcn_s_waitcnt(0);  // this lane's obs stores have landed
+  __threadfence();
+  if (mine) {
+#pragma unroll 8
+    for (int k = 0; k < NOBS; k++) stf(tobs, k, vo, ldf(obs, k, vo));
+  }
 }
 
 // ------------------------------------------------------------------ small helpers
@@ -272,7 +269,7 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
 __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
-                          const float ref[3], const ObsDst& dst, uint32_t vo, const EnvParams& prm) {
+                          const float ref[3], const Soa& dst, uint32_t vo, const EnvParams& prm) {
   float head[7];
   ObsOut o = observe_head(p, q, R, gx, gy, ref, head, prm);
   STAMP(11);
@@ -1368,7 +1365,7 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
   for (int k = 0; k < 3; k++) stf(state, ST_REF + k, vo, ref[k]);
   stf(state, ST_STEP, vo, __uint_as_float(0u));
   stf(state, ST_EPIS, vo, __uint_as_float(episode));
-  observe(qpos, q, R, gx, gy, ref, ObsDst{obs, obs, false}, vo, prm);
+  observe(qpos, q, R, gx, gy, ref, obs, vo, prm);
 }
 
 }  // namespace ak
@@ -1452,8 +1449,8 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     const bool done_pre = oh.term || trunc;
     const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
     const Soa obs = soa(A.obs, NOBS, n);
-    const ObsDst dst{obs, soa(A.tobs, NOBS, n), autoreset && A.tobs};
-    ObsOut o = observe(p, q, R, gx, gy, ref, dst, vo, A.prm);
+    ObsOut o = observe(p, q, R, gx, gy, ref, obs, vo, A.prm);
+    if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset);
     stf(soa(A.reward, 1, n), 0, vo, o.reward);
     stb(soa(A.term, 1, n, 1), (uint32_t)e, o.term ? 1 : 0);
     stb(soa(A.trunc, 1, n, 1), (uint32_t)e, trunc ? 1 : 0);
