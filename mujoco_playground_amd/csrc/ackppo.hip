@@ -23,6 +23,13 @@
 
 #include "../../include/ackppo.h"
 
+#ifndef PP_UNROLL
+#define PP_UNROLL 2
+#endif
+#define PP_STR2(x) #x
+#define PP_STR(x) PP_STR2(x)
+#define PP_UNROLL_STR PP_STR(unroll PP_UNROLL)
+
 namespace pp {
 
 constexpr int NOBS = ACKPPO_NOBS, NA = ACKPPO_NACT, H = ACKPPO_HIDDEN, P = ACKPPO_NPARAM;
@@ -53,7 +60,7 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 template <int IN>
 __device__ __forceinline__ void dense_tanh(const float* __restrict__ W, const float* __restrict__ b,
                                            const float (&x)[IN], float* col, int cs) {
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
   for (int j = 0; j < H; j++) {
     float acc = 0.0f;
 #pragma unroll
@@ -167,7 +174,7 @@ __device__ __forceinline__ void policy_trunks(PolicyLds& L, const float (&x)[NOB
   if (mine) {
     const float* W1 = L.w + net.w1;
     const float* b1 = L.w + net.b1;
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
     for (int u = u0; u < u0 + 32; u++) {
       float acc = 0.0f;
 #pragma unroll
@@ -182,7 +189,7 @@ __device__ __forceinline__ void policy_trunks(PolicyLds& L, const float (&x)[NOB
     for (int k = 0; k < H; k++) h[k] = L.h1[(hrow + k) * PT_ENVS + lane];
     const float* W2 = L.w + net.w2;
     const float* b2 = L.w + net.b2;
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
     for (int u = u0; u < u0 + 32; u++) {
       float acc = 0.0f;
 #pragma unroll
@@ -478,7 +485,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     float x[NOBS];
     load_col(tl + T_X + lane, LDP, x);
     const float* W1 = p + net.w1;
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
     for (int u = u0; u < u0 + 32; u++) {
       float acc = 0.0f;
 #pragma unroll
@@ -491,7 +498,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     float h[H];
     load_col(nt + T_H1 + lane, LDP, h);
     const float* W2 = p + net.w2;
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
     for (int u = u0; u < u0 + 32; u++) {
       float acc = 0.0f;
 #pragma unroll
@@ -560,7 +567,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
 #pragma unroll
     for (int k = 0; k < 32; k++) d1[k] = 0.0f;
     const float* W2 = p + net.w2 + u0;
-#pragma unroll 2
+_Pragma(PP_UNROLL_STR)
     for (int j = 0; j < H; j++) {
       const float dj = nt[T_D2 + j * LDP + lane];
 #pragma unroll

@@ -169,3 +169,41 @@ def test_ppo_learn_end_to_end():
     assert lg["rollout/episodes_total"] >= 256  # every env truncated at 64 steps at least once in 96
     a, _ = model.predict(venv.sim.obs_soa.t(), deterministic=True)
     assert a.shape == (256, 2) and float(a.abs().max()) <= 1.0
+
+
+def _ppo_rank(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from mujoco_playground_amd import shard
+    from mujoco_playground_amd.rl import AckermannVecEnv
+    from mujoco_playground_amd.rl.ppo import PPO
+    shard.init(backend="gloo")  # both ranks share cuda:0 here; on a node each rank owns a GPU (RCCL)
+    venv = AckermannVecEnv(128, device="cuda:0", seed=0, contacts=True, env_offset=shard.env_offset(rank, 128))
+    model = PPO("MlpPolicy", venv, n_steps=8, batch_size=256, n_epochs=2, seed=rank + 1)  # rank-dependent init ...
+    model.learn(total_timesteps=2 * 8 * 128 * world)
+    q.put((rank, model.params.cpu().numpy(), model.adam_step, model.num_timesteps))
+    dist.destroy_process_group()
+
+
+def test_ppo_data_parallel_two_ranks():
+    """DP PPO: rank 0's parameters are broadcast once and every minibatch gradient is summed over
+    ranks, so both ranks hold bit-identical parameters after learning."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ppo_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    (_, p0, s0, n0), (_, p1, s1, n1) = res
+    assert np.isfinite(p0).all() and np.array_equal(p0, p1)  # ... yet identical after the broadcast + all-reduce
+    assert s0 == s1 == 2 * 2 * (8 * 128 // 256) and n0 == n1 == 2 * 8 * 128 * 2

@@ -41,7 +41,12 @@ def _worker(rank, world, port, q):
     g = shard.gather_episode_stats(ep, w)
     s = shard.summarize_returns(g)
     m = shard.max_over_ranks(float(r + 1) * 0.5, w, torch.device("cpu"))
-    q.put((r, shard.env_offset(r, n), tuple(g.shape), s, m))
+    # the PPO learner's collectives: gradient all-reduce (SUM) and the initial parameter broadcast
+    grad = torch.full((5,), float(r + 1))
+    shard.all_reduce_sum_(grad, w)
+    params = torch.full((3,), float(10 * r + 7))
+    shard.broadcast_(params, w)
+    q.put((r, shard.env_offset(r, n), tuple(g.shape), s, m, grad.tolist(), params.tolist()))
     dist.destroy_process_group()
 
 
@@ -55,7 +60,9 @@ def test_sharded_gather_gloo_world2():
     res = sorted(q.get(timeout=120) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    (r0, off0, sh0, s0, m0), (r1, off1, sh1, s1, m1) = res
+    (r0, off0, sh0, s0, m0, g0, p0), (r1, off1, sh1, s1, m1, g1, p1) = res
+    assert g0 == g1 == [3.0] * 5          # 1 + 2 summed over ranks
+    assert p0 == p1 == [7.0] * 3          # rank 0's parameters everywhere
     assert (off0, off1) == (0, 8)
     assert sh0 == sh1 == (2, 4, 8)
     total = sum(range(8)) + sum(100 + i for i in range(8))

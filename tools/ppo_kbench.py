@@ -1,0 +1,65 @@
+"""Time the PPO kernels of one or more libackppo builds (event-timed, B=8192 minibatch, 4096 envs).
+    python tools/ppo_kbench.py path/to/libackppo.so [...]"""
+import ctypes as C
+import sys
+
+import numpy as np
+import torch
+
+NP = 18764
+dev = torch.device("cuda:0")
+
+
+def P(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def run(path):
+    L = C.CDLL(path)
+    p32, i32, f32, u32, u64, i64 = C.c_void_p, C.c_int, C.c_float, C.c_uint32, C.c_uint64, C.c_int64
+    L.ackppo_act.argtypes = [p32, p32, i32, i64, u64, u32, i32, p32, p32, p32, p32, p32, p32]
+    L.ackppo_grad.argtypes = [p32] * 7 + [i32, p32, f32, f32, f32, p32, p32, p32]
+    L.ackppo_reduce.argtypes = [p32, p32, i32, f32, p32, p32, p32]
+    L.ackppo_adam.argtypes = [p32, p32, p32, p32, f32, f32, f32, f32, f32, f32, f32, p32, p32]
+    g = torch.Generator(device="cpu").manual_seed(0)
+    params = (torch.randn(NP, generator=g) * 0.1).to(dev)
+    S, B, N = 131072, 8192, 4096
+    obs = torch.randn(S, 79, device=dev)
+    act = torch.randn(S, 2, device=dev)
+    lp = torch.randn(S, device=dev)
+    adv = torch.randn(S, device=dev)
+    ret = torch.randn(S, device=dev)
+    idx = torch.randperm(S, device=dev).to(torch.int32)
+    stats = torch.tensor([0.0, 1.0], device=dev)
+    nblk = B // 64
+    gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
+    grad, loss = torch.zeros(NP, device=dev), torch.zeros(8, device=dev)
+    m, v, nrm = torch.zeros(NP, device=dev), torch.zeros(NP, device=dev), torch.zeros(1, device=dev)
+    obs_soa = torch.randn(79, N, device=dev)
+    ea, a2, l2, v2 = (torch.zeros(N, 2, device=dev), torch.zeros(N, 2, device=dev), torch.zeros(N, device=dev),
+                      torch.zeros(N, device=dev))
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = {}
+    for name, fn in [
+        ("grad", lambda: L.ackppo_grad(P(params), P(obs), P(act), P(lp), P(adv), P(ret), P(idx), B, P(stats), 0.2, 0.0,
+                                       0.5, P(gp), P(lpart), s)),
+        ("reduce", lambda: L.ackppo_reduce(P(gp), P(lpart), nblk, 0.0, P(grad), P(loss), s)),
+        ("adam", lambda: L.ackppo_adam(P(params), P(grad), P(m), P(v), 1.0, 0.5, 0.9, 0.999, 1e-5, 3e-4, 0.03,
+                                       P(nrm), s)),
+        ("act", lambda: L.ackppo_act(P(params), P(obs_soa), N, 0, 1, 2, 0, None, P(a2), P(ea), P(l2), P(v2), s)),
+    ]:
+        for _ in range(3):
+            assert fn() == 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(20):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = round(e0.elapsed_time(e1) / 20 * 1000, 1)
+    print(path, res, "grad checksum", float(grad.abs().sum()), flush=True)
+
+
+for p in sys.argv[1:]:
+    run(p)
