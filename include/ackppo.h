@@ -51,7 +51,6 @@ extern "C" {
 #define ACKPPO_OFF_VAL_W 18696    /* value_net.weight                  [1][64]  */
 #define ACKPPO_OFF_VAL_B 18760    /* value_net.bias                    [1]     */
 #define ACKPPO_NPARAM 18764
-#define ACKPPO_TILE 64            /* samples per ackppo_grad workgroup (one partial row each) */
 #define ACKPPO_NLOSS 8            /* loss partial words per workgroup (see ackppo_grad) */
 
 #define ACKPPO_OK 0
@@ -91,9 +90,9 @@ int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int
                      float* stats, void* stream);
 
 /* Gradient of the PPO loss of one minibatch (samples idx[0..batch)), split over
- * ceil(batch / ACKPPO_TILE) workgroups, each writing its row of grad_partial [nblk][NPARAM]
- * (pad words are never written: zero them once) and loss_partial [nblk][8] =
- * (sum pg_loss, sum (R-V)^2, n clipped, sum approx_kl, n samples, 0, 0, 0).
+ * nblk = ackppo_grad_blocks(batch) workgroups (one per CU at most), each writing its row of
+ * grad_partial [nblk][NPARAM] (pad words are never written: zero them once) and of
+ * loss_partial [nblk][8] = (sum pg_loss, sum (R-V)^2, n clipped, sum approx_kl, n samples, 0, 0, 0).
  * stats: (mean, inv_std) of this minibatch (ackppo_adv_stats). The entropy term is
  * sample-independent and is added by ackppo_reduce. */
 int ackppo_grad(const float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
@@ -101,7 +100,10 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
                 float clip_range, float ent_coef, float vf_coef, float* grad_partial, float* loss_partial,
                 void* stream);
 
-/* grad [NPARAM] = sum of nblk partial rows; d(-ent_coef * entropy)/d log_std = -ent_coef added;
+/* Number of partial rows ackppo_grad writes for a minibatch of `batch` samples. */
+int ackppo_grad_blocks(int batch);
+
+/* grad [NPARAM] = sum of nblk partial rows (grad is overwritten); d(-ent_coef * entropy)/d log_std = -ent_coef added;
  * loss [8] = column sums of loss_partial. */
 int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream);

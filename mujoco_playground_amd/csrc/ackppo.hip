@@ -30,11 +30,23 @@
 #define PP_STR(x) PP_STR2(x)
 #define PP_UNROLL_STR PP_STR(unroll PP_UNROLL)
 
+#ifdef PP_STAMPS
+__device__ unsigned long long* g_pp_stamps;
+#define PSTAMP(k)                                                                              \
+  do {                                                                                         \
+    unsigned long long _t;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");               \
+    if (threadIdx.x == 0) g_pp_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;                 \
+  } while (0)
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 namespace pp {
 
 constexpr int NOBS = ACKPPO_NOBS, NA = ACKPPO_NACT, H = ACKPPO_HIDDEN, P = ACKPPO_NPARAM;
-constexpr int TILE = ACKPPO_TILE;
-constexpr int LDP = 68;  // LDS row stride of the grad tiles: 16-B aligned rows, 4-bank skew per row
 constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;
 constexpr float TWO_PI = 6.28318530717958647692f;
 
@@ -388,56 +400,88 @@ struct GradArgs {
   float* lpart;
 };
 
-// LDS map of one tile (floats, rows of LDP): X [80 rows], then per net h1, h2, d2, d1 [64 rows each],
-// then gmu [2], glog [2], gv [1] rows.
-constexpr int T_X = 0, T_NET = 80 * LDP, NET_SZ = 4 * H * LDP;
-constexpr int T_H1 = 0, T_H2 = H * LDP, T_D2 = 2 * H * LDP, T_D1 = 3 * H * LDP;
-constexpr int T_VEC = T_NET + 2 * NET_SZ;
-constexpr int T_GMU = T_VEC, T_GLOG = T_VEC + 2 * LDP, T_GV = T_VEC + 4 * LDP;
-constexpr int T_TOTAL = T_VEC + 5 * LDP;
-static_assert(T_TOTAL * 4 <= 160 * 1024, "grad tile exceeds the 160 KiB LDS of a CU");
+// ---- ackppo_grad LDS map (floats). Weights: staged once per workgroup, the first layers
+// transposed ([k][unit], so a lane's 16 units are 4 contiguous 16-B reads), the second layers
+// row-major. Tile: GT samples, rows of GLDP floats (16-B aligned): X [80 rows], per net
+// h1, h2, d2, d1 [64 rows each], then gmu [2], glog [2], gv [1] rows.
+constexpr int GT = 32, GLDP = 36;
+constexpr int W_W1T = 0, W_W2_A = 160 * H, W_W2_C = W_W2_A + H * H;  // W1T: [80][128] = [k][actor|critic unit]
+constexpr int W_B1_A = W_W2_C + H * H, W_B2_A = W_B1_A + H, W_B1_C = W_B2_A + H, W_B2_C = W_B1_C + H;
+constexpr int W_AW = W_B2_C + H, W_AB = W_AW + 2 * H, W_CW = W_AB + 4, W_CB = W_CW + H, W_LS = W_CB + 4;
+constexpr int W_TOTAL = W_LS + 4;
+constexpr int G_X = W_TOTAL, G_NET = G_X + 80 * GLDP, G_NETSZ = 4 * H * GLDP;
+constexpr int G_H1 = 0, G_H2 = H * GLDP, G_D2 = 2 * H * GLDP, G_D1 = 3 * H * GLDP;
+constexpr int G_VEC = G_NET + 2 * G_NETSZ;
+constexpr int G_GMU = G_VEC, G_GLOG = G_VEC + 2 * GLDP, G_GV = G_VEC + 4 * GLDP;
+constexpr int G_TOTAL = G_VEC + 5 * GLDP;
+static_assert(G_TOTAL * 4 <= 160 * 1024, "grad workgroup exceeds the 160 KiB LDS of a CU");
 constexpr int GRAD_THREADS = 256;
+constexpr int GRAD_MAX_BLOCKS = 256;  // one workgroup per CU (the LDS footprint allows one)
 
-// sum over the tile's samples of a[ra][s] * b[rb][s] for a 4x4 block of rows (16-B LDS reads)
-__device__ __forceinline__ void outer4x4(const float* a, const float* b, float acc[4][4]) {
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++) acc[i][j] = 0.0f;
-#pragma unroll 4
-  for (int s = 0; s < TILE; s += 4) {
+__device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, float* w) {
+  // transposed first layers, both nets side by side (k row 79 = 0); consecutive threads write
+  // consecutive LDS words
+  for (int i = threadIdx.x; i < 80 * 2 * H; i += GRAD_THREADS) {
+    const int k = i / (2 * H), c = i - k * 2 * H, net = c >> 6, u = c & 63;
+    const int src = (net == 0 ? ACKPPO_OFF_PI_W1 : ACKPPO_OFF_VF_W1) + u * NOBS + k;
+    w[W_W1T + i] = k < NOBS ? p[src] : 0.0f;
+  }
+  for (int i = threadIdx.x; i < H * H; i += GRAD_THREADS) {
+    w[W_W2_A + i] = p[ACKPPO_OFF_PI_W2 + i];
+    w[W_W2_C + i] = p[ACKPPO_OFF_VF_W2 + i];
+  }
+  for (int i = threadIdx.x; i < H; i += GRAD_THREADS) {
+    w[W_B1_A + i] = p[ACKPPO_OFF_PI_B1 + i];
+    w[W_B2_A + i] = p[ACKPPO_OFF_PI_B2 + i];
+    w[W_B1_C + i] = p[ACKPPO_OFF_VF_B1 + i];
+    w[W_B2_C + i] = p[ACKPPO_OFF_VF_B2 + i];
+    w[W_AW + i] = p[ACKPPO_OFF_ACT_W + i];
+    w[W_AW + H + i] = p[ACKPPO_OFF_ACT_W + H + i];
+    w[W_CW + i] = p[ACKPPO_OFF_VAL_W + i];
+  }
+  if (threadIdx.x < 2) {
+    w[W_AB + threadIdx.x] = p[ACKPPO_OFF_ACT_B + threadIdx.x];
+    w[W_LS + threadIdx.x] = p[ACKPPO_OFF_LOG_STD + threadIdx.x];
+  }
+  if (threadIdx.x == 0) w[W_CB] = p[ACKPPO_OFF_VAL_B];
+}
+
+// sum over the GT samples of a[r][s] * b[c][s] for a 4x4 block of rows, added into acc
+__device__ __forceinline__ void outer4x4_acc(const float* a, const float* b, float acc[16]) {
+#pragma unroll 2
+  for (int s = 0; s < GT; s += 4) {
     float4 av[4], bv[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      av[i] = *reinterpret_cast<const float4*>(a + i * LDP + s);
-      bv[i] = *reinterpret_cast<const float4*>(b + i * LDP + s);
+      av[i] = *reinterpret_cast<const float4*>(a + i * GLDP + s);
+      bv[i] = *reinterpret_cast<const float4*>(b + i * GLDP + s);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        acc[i][j] = fmaf(av[i].x, bv[j].x, acc[i][j]);
-        acc[i][j] = fmaf(av[i].y, bv[j].y, acc[i][j]);
-        acc[i][j] = fmaf(av[i].z, bv[j].z, acc[i][j]);
-        acc[i][j] = fmaf(av[i].w, bv[j].w, acc[i][j]);
+        float t = acc[4 * i + j];
+        t = fmaf(av[i].x, bv[j].x, t);
+        t = fmaf(av[i].y, bv[j].y, t);
+        t = fmaf(av[i].z, bv[j].z, t);
+        t = fmaf(av[i].w, bv[j].w, t);
+        acc[4 * i + j] = t;
       }
   }
 }
-
-__device__ __forceinline__ float row_sum(const float* a) {
+__device__ __forceinline__ float row_sum_g(const float* a) {
   float s = 0.0f;
-#pragma unroll 4
-  for (int i = 0; i < TILE; i += 4) {
+#pragma unroll
+  for (int i = 0; i < GT; i += 4) {
     const float4 v = *reinterpret_cast<const float4*>(a + i);
     s += (v.x + v.y) + (v.z + v.w);
   }
   return s;
 }
-
-__device__ __forceinline__ float row_dot(const float* a, const float* b) {
+__device__ __forceinline__ float row_dot_g(const float* a, const float* b) {
   float s = 0.0f;
-#pragma unroll 4
-  for (int i = 0; i < TILE; i += 4) {
+#pragma unroll
+  for (int i = 0; i < GT; i += 4) {
     const float4 u = *reinterpret_cast<const float4*>(a + i), v = *reinterpret_cast<const float4*>(b + i);
     s = fmaf(u.x, v.x, s);
     s = fmaf(u.y, v.y, s);
@@ -447,216 +491,339 @@ __device__ __forceinline__ float row_dot(const float* a, const float* b) {
   return s;
 }
 
+// weight-gradient work items of one thread: first-layer 4x4 blocks (2 nets x 16 x 20 = 640),
+// second-layer 4x4 blocks (2 x 16 x 16 = 512), vector entries (453; see vec_item)
+constexpr int NB1 = 640, NB2 = 512, NVEC = 453;
+constexpr int PER1 = (NB1 + GRAD_THREADS - 1) / GRAD_THREADS, PER2 = NB2 / GRAD_THREADS;
+constexpr int PERV = (NVEC + GRAD_THREADS - 1) / GRAD_THREADS;
+
+__device__ __forceinline__ float vec_item(const float* tl, int i) {
+  const float* an = tl + G_NET;
+  const float* cn = tl + G_NET + G_NETSZ;
+  if (i < 64) return row_sum_g(an + G_D1 + i * GLDP);
+  if (i < 128) return row_sum_g(an + G_D2 + (i - 64) * GLDP);
+  if (i < 192) return row_sum_g(cn + G_D1 + (i - 128) * GLDP);
+  if (i < 256) return row_sum_g(cn + G_D2 + (i - 192) * GLDP);
+  if (i < 384) {
+    const int d = (i - 256) >> 6, j = (i - 256) & 63;
+    return row_dot_g(tl + G_GMU + d * GLDP, an + G_H2 + j * GLDP);
+  }
+  if (i < 386) return row_sum_g(tl + G_GMU + (i - 384) * GLDP);
+  if (i < 450) return row_dot_g(tl + G_GV, cn + G_H2 + (i - 386) * GLDP);
+  if (i == 450) return row_sum_g(tl + G_GV);
+  return row_sum_g(tl + G_GLOG + (i - 451) * GLDP);
+}
+__device__ __forceinline__ int vec_offset(int i) {
+  if (i < 64) return ACKPPO_OFF_PI_B1 + i;
+  if (i < 128) return ACKPPO_OFF_PI_B2 + i - 64;
+  if (i < 192) return ACKPPO_OFF_VF_B1 + i - 128;
+  if (i < 256) return ACKPPO_OFF_VF_B2 + i - 192;
+  if (i < 384) return ACKPPO_OFF_ACT_W + (i - 256);
+  if (i < 386) return ACKPPO_OFF_ACT_B + i - 384;
+  if (i < 450) return ACKPPO_OFF_VAL_W + i - 386;
+  if (i == 450) return ACKPPO_OFF_VAL_B;
+  return ACKPPO_OFF_LOG_STD + i - 451;
+}
+
+// One workgroup per CU; workgroup b processes tiles b, b + grid, ... of GT samples and keeps its
+// weight gradients in registers across tiles, writing one partial row at the end.
 extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(GradArgs A) {
+  PSTAMP(0);
   extern __shared__ float tl[];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar weight loads below
-  const int blk = blockIdx.x;
-  const int s0 = blk * TILE;
-  const int nvalid = min(TILE, A.batch - s0);
-  const float* __restrict__ p = A.params;
-
-  // cooperative gather of the tile's observation rows into X [k][s] (zero rows for padding):
-  // thread t copies a quarter row (20 words) with all its loads in flight at once
-  {
-    const int s = tid >> 2, q = tid & 3;
-    const bool ok = s < nvalid;
-    const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + s] : 0) * NOBS;
-    float v[20];
-#pragma unroll
-    for (int i = 0; i < 20; i++) {
-      const int k = q * 20 + i;
-      v[i] = (ok && k < NOBS) ? row[k] : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < 20; i++) tl[T_X + (q * 20 + i) * LDP + s] = v[i];
-  }
-  __syncthreads();
-
-  // ---- per-sample forward / loss gradient / backward. lane = sample; wave w works on net
-  // (w >> 1) (0 actor, 1 critic) and on units [32 (w & 1), +32) of each of its layers.
-  const bool valid = lane < nvalid;
-  const int sidx = valid ? A.idx[s0 + lane] : 0;
-  const int nid = wave >> 1, u0 = (wave & 1) * 32;
-  const Net net = nid == 0 ? ACTOR : CRITIC;
-  float* nt = tl + T_NET + nid * NET_SZ;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = lane & 31, uh = lane >> 5;            // per-sample phases: sample in tile, lane half
+  const int nid = wave >> 1;                          // 0 actor, 1 critic
+  float* w = tl;
+  float* nt = tl + G_NET + nid * G_NETSZ;
   const float invB = 1.0f / (float)A.batch;
-  {  // layer 1
-    float x[NOBS];
-    load_col(tl + T_X + lane, LDP, x);
-    const float* W1 = p + net.w1;
-_Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + 32; u++) {
-      float acc = 0.0f;
+  stage_grad_weights(A.params, w);
+
+  float acc1[PER1][16], acc2[PER2][16], accv[PERV];
 #pragma unroll
-      for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
-      nt[T_H1 + u * LDP + lane] = tanhf(acc + p[net.b1 + u]);
-    }
-  }
-  __syncthreads();
-  {  // layer 2
-    float h[H];
-    load_col(nt + T_H1 + lane, LDP, h);
-    const float* W2 = p + net.w2;
-_Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + 32; u++) {
-      float acc = 0.0f;
+  for (int b = 0; b < PER1; b++)
 #pragma unroll
-      for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
-      nt[T_H2 + u * LDP + lane] = tanhf(acc + p[net.b2 + u]);
-    }
-  }
-  __syncthreads();
-  // heads and the loss gradient w.r.t. their outputs (waves 0 and 2)
-  float loss_a = 0.0f, loss_b = 0.0f, loss_c = 0.0f;
-  if (wave == 0) {
-    float h[H], mu[NA], a[NA];
-    load_col(nt + T_H2 + lane, LDP, h);
-    actor_head(p, h, mu);
-    a[0] = A.actions[2 * (size_t)sidx];
-    a[1] = A.actions[2 * (size_t)sidx + 1];
-    const float logp = gauss_logp(a, mu, p);
-    const float lr = logp - A.old_logp[sidx];
-    const float r = expf(lr);
-    const float adv = (A.adv[sidx] - A.stats[0]) * A.stats[1];
-    const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
-    const float l1 = adv * r, l2 = adv * rc;
-    // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
-    // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
-    const float glogp = valid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
+    for (int i = 0; i < 16; i++) acc1[b][i] = 0.0f;
 #pragma unroll
-    for (int d = 0; d < NA; d++) {
-      const float sigma = expf(p[ACKPPO_OFF_LOG_STD + d]);
-      const float dv = a[d] - mu[d];
-      tl[T_GMU + d * LDP + lane] = glogp * dv / (sigma * sigma);
-      tl[T_GLOG + d * LDP + lane] = glogp * (dv * dv / (sigma * sigma) - 1.0f);
+  for (int b = 0; b < PER2; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc2[b][i] = 0.0f;
+#pragma unroll
+  for (int b = 0; b < PERV; b++) accv[b] = 0.0f;
+  float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
+
+  const int ntiles = (A.batch + GT - 1) / GT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
+    __syncthreads();  // previous tile's LDS reads are done (and the weights are staged)
+    {  // gather: thread t copies 10 words of row (t >> 3)
+      const int r = tid >> 3, q = tid & 7;
+      const bool ok = r < nvalid;
+      const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + r] : 0) * NOBS;
+      float v[10];
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+        const int k = q * 10 + i;
+        v[i] = (ok && k < NOBS) ? row[k] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < 10; i++) tl[G_X + (q * 10 + i) * GLDP + r] = v[i];
     }
-    if (valid) {
-      loss_a = -fminf(l1, l2);
-      loss_b = (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
-      loss_c = (r - 1.0f) - lr;
-    }
-  } else if (wave == 2) {
-    float h[H];
-    load_col(nt + T_H2 + lane, LDP, h);
-    const float v = critic_head(p, h);
-    const float R = A.ret[sidx];
-    tl[T_GV + lane] = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
-    if (valid) loss_a = (R - v) * (R - v);
-  }
-  __syncthreads();
-  // d2[u] = (dL/dh2[u]) (1 - h2[u]^2) for this wave's units
-  if (nid == 0) {
-    const float g0 = tl[T_GMU + lane], g1 = tl[T_GMU + LDP + lane];
+    __syncthreads();
+    PSTAMP(1);
+    const bool valid = s < nvalid;
+    const int sidx = valid ? A.idx[s0 + s] : 0;
+    // GEMM-shaped layers: thread (ub, sb) owns 4 units (of the 128 actor|critic units) x 4 samples
+    const int ub = tid >> 3, sb = tid & 7, gnet = ub >> 4, gu = 4 * (ub & 15), gs = 4 * sb;
+    float* gt = tl + G_NET + gnet * G_NETSZ;  // this thread's net tile
+    {  // layer 1: H1 = tanh(W1 X + b1), k-outer, two 16-B LDS reads per 16 FMAs
+      float acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
 #pragma unroll 4
-    for (int u = u0; u < u0 + 32; u++) {
-      const float hu = nt[T_H2 + u * LDP + lane];
-      nt[T_D2 + u * LDP + lane] = (g0 * p[ACKPPO_OFF_ACT_W + u] + g1 * p[ACKPPO_OFF_ACT_W + H + u]) * (1.0f - hu * hu);
-    }
-  } else {
-    const float gv = tl[T_GV + lane];
-#pragma unroll 4
-    for (int u = u0; u < u0 + 32; u++) {
-      const float hu = nt[T_H2 + u * LDP + lane];
-      nt[T_D2 + u * LDP + lane] = gv * p[ACKPPO_OFF_VAL_W + u] * (1.0f - hu * hu);
-    }
-  }
-  __syncthreads();
-  {  // d1[k] = (sum_j d2[j] W2[j][k]) (1 - h1[k]^2) for this wave's k in [u0, u0+32)
-    float d1[32];
+      for (int k = 0; k < 80; k++) {
+        const float4 wv = *reinterpret_cast<const float4*>(w + W_W1T + k * 2 * H + 4 * ub);
+        const float4 xv = *reinterpret_cast<const float4*>(tl + G_X + k * GLDP + gs);
+        const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-    for (int k = 0; k < 32; k++) d1[k] = 0.0f;
-    const float* W2 = p + net.w2 + u0;
-_Pragma(PP_UNROLL_STR)
-    for (int j = 0; j < H; j++) {
-      const float dj = nt[T_D2 + j * LDP + lane];
+        for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int k = 0; k < 32; k++) d1[k] = fmaf(dj, W2[j * H + k], d1[k]);
-    }
+          for (int j = 0; j < 4; j++) acc[4 * i + j] = fmaf(wa[i], xa[j], acc[4 * i + j]);
+      }
+      const float* b1 = w + (gnet == 0 ? W_B1_A : W_B1_C);
 #pragma unroll
-    for (int k = 0; k < 32; k++) {
-      const float hk = nt[T_H1 + (u0 + k) * LDP + lane];
-      nt[T_D1 + (u0 + k) * LDP + lane] = d1[k] * (1.0f - hk * hk);
-    }
-  }
-  // loss statistics of the tile (waves 0 and 2 hold them)
-  if (wave == 0 || wave == 2) {
-    loss_a = wave_sum(loss_a);
-    loss_b = wave_sum(loss_b);
-    loss_c = wave_sum(loss_c);
-    if (lane == 0) {
-      float* lp = A.lpart + (size_t)blk * ACKPPO_NLOSS;
-      if (wave == 0) {
-        lp[0] = loss_a;
-        lp[2] = loss_b;
-        lp[3] = loss_c;
-        lp[4] = (float)nvalid;
-        lp[5] = lp[6] = lp[7] = 0.0f;
-      } else {
-        lp[1] = loss_a;
+      for (int i = 0; i < 4; i++) {
+        const float4 o = make_float4(tanhf(acc[4 * i] + b1[gu + i]), tanhf(acc[4 * i + 1] + b1[gu + i]),
+                                     tanhf(acc[4 * i + 2] + b1[gu + i]), tanhf(acc[4 * i + 3] + b1[gu + i]));
+        *reinterpret_cast<float4*>(gt + G_H1 + (gu + i) * GLDP + gs) = o;
       }
     }
-  }
-  __syncthreads();
-
-  // ---- weight gradients: sums over the tile of outer products (all waves, both nets)
-  float* g = A.gpart + (size_t)blk * P;
-  // layer 1: [64 units][79 inputs] per net as 4x4 blocks (16 x 20 blocks per net)
-  for (int b = tid; b < 2 * 16 * 20; b += GRAD_THREADS) {
-    const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
-    const float* net_t = tl + T_NET + nn * NET_SZ;
-    float acc[4][4];
-    outer4x4(net_t + T_D1 + 4 * jb * LDP, tl + T_X + 4 * kb * LDP, acc);
-    const int w1 = nn == 0 ? ACKPPO_OFF_PI_W1 : ACKPPO_OFF_VF_W1;
+    __syncthreads();
+    PSTAMP(2);
+    {  // layer 2: H2 = tanh(W2 H1 + b2) per net (row-major W2: four 4-B reads + one 16-B read per 16 FMAs)
+      float acc[16];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+      const float* W2 = w + (gnet == 0 ? W_W2_A : W_W2_C) + gu * H;
+#pragma unroll 4
+      for (int k = 0; k < H; k++) {
+        const float4 hv = *reinterpret_cast<const float4*>(gt + G_H1 + k * GLDP + gs);
+        const float wa[4] = {W2[k], W2[H + k], W2[2 * H + k], W2[3 * H + k]}, ha[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (4 * kb + j < NOBS) g[w1 + (4 * jb + i) * NOBS + 4 * kb + j] = acc[i][j];
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int j = 0; j < 4; j++) acc[4 * i + j] = fmaf(wa[i], ha[j], acc[4 * i + j]);
+      }
+      const float* b2 = w + (gnet == 0 ? W_B2_A : W_B2_C);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float4 o = make_float4(tanhf(acc[4 * i] + b2[gu + i]), tanhf(acc[4 * i + 1] + b2[gu + i]),
+                                     tanhf(acc[4 * i + 2] + b2[gu + i]), tanhf(acc[4 * i + 3] + b2[gu + i]));
+        *reinterpret_cast<float4*>(gt + G_H2 + (gu + i) * GLDP + gs) = o;
+      }
+    }
+    __syncthreads();
+    PSTAMP(3);
+    if (uh == 0 && (wave & 1) == 0) {  // heads + loss gradient: 32 lanes of waves 0 (actor) and 2 (critic)
+      float h[H];
+#pragma unroll
+      for (int k = 0; k < H; k++) h[k] = nt[G_H2 + k * GLDP + s];
+      if (nid == 0) {
+        float mu[NA], a[NA];
+#pragma unroll
+        for (int d = 0; d < NA; d++) {
+          float m = 0.0f;
+#pragma unroll
+          for (int j = 0; j < H; j++) m = fmaf(w[W_AW + d * H + j], h[j], m);
+          mu[d] = m + w[W_AB + d];
+        }
+        a[0] = A.actions[2 * (size_t)sidx];
+        a[1] = A.actions[2 * (size_t)sidx + 1];
+        float logp = 0.0f;
+#pragma unroll
+        for (int d = 0; d < NA; d++) {
+          const float sigma = expf(w[W_LS + d]);
+          const float dv = a[d] - mu[d];
+          logp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
+        }
+        const float lr = logp - A.old_logp[sidx];
+        const float r = expf(lr);
+        const float adv = (A.adv[sidx] - A.stats[0]) * A.stats[1];
+        const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
+        const float l1 = adv * r, l2 = adv * rc;
+        // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
+        // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
+        const float glogp = valid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
+#pragma unroll
+        for (int d = 0; d < NA; d++) {
+          const float sigma = expf(w[W_LS + d]);
+          const float dv = a[d] - mu[d];
+          tl[G_GMU + d * GLDP + s] = glogp * dv / (sigma * sigma);
+          tl[G_GLOG + d * GLDP + s] = glogp * (dv * dv / (sigma * sigma) - 1.0f);
+        }
+        if (valid) {
+          la += -fminf(l1, l2);
+          lb += (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
+          lc += (r - 1.0f) - lr;
+          ln += 1.0f;
+        }
+      } else {
+        float v = 0.0f;
+#pragma unroll
+        for (int j = 0; j < H; j++) v = fmaf(w[W_CW + j], h[j], v);
+        v += w[W_CB];
+        const float R = A.ret[sidx];
+        tl[G_GV + s] = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
+        if (valid) la += (R - v) * (R - v);
+      }
+    }
+    __syncthreads();
+    PSTAMP(4);
+    {  // d2 = (dL/dh2) (1 - h2^2) for this thread's 4 units x 4 samples
+      const float4 hv0 = *reinterpret_cast<const float4*>(tl + G_GMU + gs);
+      const float4 hv1 = *reinterpret_cast<const float4*>(tl + G_GMU + GLDP + gs);
+      const float4 gvv = *reinterpret_cast<const float4*>(tl + G_GV + gs);
+      const float g0[4] = {hv0.x, hv0.y, hv0.z, hv0.w}, g1[4] = {hv1.x, hv1.y, hv1.z, hv1.w};
+      const float gv[4] = {gvv.x, gvv.y, gvv.z, gvv.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int u = gu + i;
+        const float4 h2 = *reinterpret_cast<const float4*>(gt + G_H2 + u * GLDP + gs);
+        const float ha[4] = {h2.x, h2.y, h2.z, h2.w};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float dh = gnet == 0 ? g0[j] * w[W_AW + u] + g1[j] * w[W_AW + H + u] : gv[j] * w[W_CW + u];
+          o[j] = dh * (1.0f - ha[j] * ha[j]);
+        }
+        *reinterpret_cast<float4*>(gt + G_D2 + u * GLDP + gs) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    __syncthreads();
+    PSTAMP(5);
+    {  // d1 = (W2^T d2) (1 - h1^2): j-outer over row-major W2, two 16-B reads per 16 FMAs
+      float acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+      const float* W2 = w + (gnet == 0 ? W_W2_A : W_W2_C) + gu;
+#pragma unroll 4
+      for (int j = 0; j < H; j++) {
+        const float4 wv = *reinterpret_cast<const float4*>(W2 + j * H);
+        const float4 dv = *reinterpret_cast<const float4*>(gt + G_D2 + j * GLDP + gs);
+        const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int jj = 0; jj < 4; jj++) acc[4 * i + jj] = fmaf(wa[i], da[jj], acc[4 * i + jj]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float4 h1 = *reinterpret_cast<const float4*>(gt + G_H1 + (gu + i) * GLDP + gs);
+        const float4 o = make_float4(acc[4 * i] * (1.0f - h1.x * h1.x), acc[4 * i + 1] * (1.0f - h1.y * h1.y),
+                                     acc[4 * i + 2] * (1.0f - h1.z * h1.z), acc[4 * i + 3] * (1.0f - h1.w * h1.w));
+        *reinterpret_cast<float4*>(gt + G_D1 + (gu + i) * GLDP + gs) = o;
+      }
+    }
+    __syncthreads();
+    PSTAMP(6);
+    // weight-gradient sums over the tile (rows of padding samples are zero)
+#pragma unroll
+    for (int bb = 0; bb < PER1; bb++) {
+      const int b = tid + bb * GRAD_THREADS;
+      if (b < NB1) {
+        const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
+        outer4x4_acc(tl + G_NET + nn * G_NETSZ + G_D1 + 4 * jb * GLDP, tl + G_X + 4 * kb * GLDP, acc1[bb]);
+      }
+    }
+#pragma unroll
+    for (int bb = 0; bb < PER2; bb++) {
+      const int b = tid + bb * GRAD_THREADS;
+      const int nn = b / 256, r = b - nn * 256, jb = r / 16, kb = r - jb * 16;
+      const float* nb = tl + G_NET + nn * G_NETSZ;
+      outer4x4_acc(nb + G_D2 + 4 * jb * GLDP, nb + G_H1 + 4 * kb * GLDP, acc2[bb]);
+    }
+#pragma unroll
+    for (int bb = 0; bb < PERV; bb++) {
+      const int i = tid + bb * GRAD_THREADS;
+      if (i < NVEC) accv[bb] += vec_item(tl, i);
+    }
   }
-  // layer 2: [64][64] per net (16 x 16 blocks per net)
-  for (int b = tid; b < 2 * 16 * 16; b += GRAD_THREADS) {
+  PSTAMP(7);
+  // this workgroup's partial gradient row and loss sums
+  float* g = A.gpart + (size_t)blockIdx.x * P;
+#pragma unroll
+  for (int bb = 0; bb < PER1; bb++) {
+    const int b = tid + bb * GRAD_THREADS;
+    if (b < NB1) {
+      const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
+      const int w1 = nn == 0 ? ACKPPO_OFF_PI_W1 : ACKPPO_OFF_VF_W1;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (4 * kb + j < NOBS) g[w1 + (4 * jb + i) * NOBS + 4 * kb + j] = acc1[bb][4 * i + j];
+    }
+  }
+#pragma unroll
+  for (int bb = 0; bb < PER2; bb++) {
+    const int b = tid + bb * GRAD_THREADS;
     const int nn = b / 256, r = b - nn * 256, jb = r / 16, kb = r - jb * 16;
-    const float* net_t = tl + T_NET + nn * NET_SZ;
-    float acc[4][4];
-    outer4x4(net_t + T_D2 + 4 * jb * LDP, net_t + T_H1 + 4 * kb * LDP, acc);
     const int w2 = nn == 0 ? ACKPPO_OFF_PI_W2 : ACKPPO_OFF_VF_W2;
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int j = 0; j < 4; j++) g[w2 + (4 * jb + i) * H + 4 * kb + j] = acc[i][j];
+      for (int j = 0; j < 4; j++) g[w2 + (4 * jb + i) * H + 4 * kb + j] = acc2[bb][4 * i + j];
   }
-  // biases, heads, log_std
-  const float* an = tl + T_NET;
-  const float* cn = tl + T_NET + NET_SZ;
-  for (int i = tid; i < 453; i += GRAD_THREADS) {
-    if (i < 64) g[ACKPPO_OFF_PI_B1 + i] = row_sum(an + T_D1 + i * LDP);
-    else if (i < 128) g[ACKPPO_OFF_PI_B2 + i - 64] = row_sum(an + T_D2 + (i - 64) * LDP);
-    else if (i < 192) g[ACKPPO_OFF_VF_B1 + i - 128] = row_sum(cn + T_D1 + (i - 128) * LDP);
-    else if (i < 256) g[ACKPPO_OFF_VF_B2 + i - 192] = row_sum(cn + T_D2 + (i - 192) * LDP);
-    else if (i < 384) {
-      const int d = (i - 256) >> 6, j = (i - 256) & 63;
-      g[ACKPPO_OFF_ACT_W + d * H + j] = row_dot(tl + T_GMU + d * LDP, an + T_H2 + j * LDP);
-    } else if (i < 386) g[ACKPPO_OFF_ACT_B + i - 384] = row_sum(tl + T_GMU + (i - 384) * LDP);
-    else if (i < 450) g[ACKPPO_OFF_VAL_W + i - 386] = row_dot(tl + T_GV, cn + T_H2 + (i - 386) * LDP);
-    else if (i == 450) g[ACKPPO_OFF_VAL_B] = row_sum(tl + T_GV);
-    else g[ACKPPO_OFF_LOG_STD + i - 451] = row_sum(tl + T_GLOG + (i - 451) * LDP);
+#pragma unroll
+  for (int bb = 0; bb < PERV; bb++) {
+    const int i = tid + bb * GRAD_THREADS;
+    if (i < NVEC) g[vec_offset(i)] = accv[bb];
   }
+  if ((wave & 1) == 0) {
+    la = wave_sum(la);
+    lb = wave_sum(lb);
+    lc = wave_sum(lc);
+    ln = wave_sum(ln);
+    if (lane == 0) {
+      float* lp = A.lpart + (size_t)blockIdx.x * ACKPPO_NLOSS;
+      if (wave == 0) {
+        lp[0] = la;
+        lp[2] = lb;
+        lp[3] = lc;
+        lp[4] = ln;
+        lp[5] = lp[6] = lp[7] = 0.0f;
+      } else {
+        lp[1] = la;
+      }
+    }
+  }
+  PSTAMP(15);
 }
 
-extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const float* gpart, const float* lpart, int nblk,
-                                                                       float ent_coef, float* grad, float* loss) {
+// Two passes, no atomics: (1) grid (param blocks of 256, REDUCE_RG row groups) sums rows
+// by, by + RG, ... into tmp[by][p] with 4 loads in flight per thread; (2) sums the RG rows.
+constexpr int REDUCE_RG = 16;
+extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(const float* gpart, int nblk, float* tmp) {
+  const int pidx = blockIdx.x * 256 + threadIdx.x;
+  const int rg = gridDim.y, by = blockIdx.y;
+  if (pidx >= P) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = by;
+  for (; b + 3 * rg < nblk; b += 4 * rg) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc[i] += gpart[(size_t)(b + i * rg) * P + pidx];
+  }
+  for (; b < nblk; b += rg) acc[0] += gpart[(size_t)b * P + pidx];
+  tmp[(size_t)by * P + pidx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const float* tmp, int rg, const float* lpart,
+                                                                       int nblk, float ent_coef, float* grad,
+                                                                       float* loss) {
   const int pidx = blockIdx.x * 256 + threadIdx.x;
   if (pidx < P) {
-    // 8 independent partial sums keep 8 row loads in flight per thread
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int b = 0;
-    for (; b + 8 <= nblk; b += 8) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) acc[i] += gpart[(size_t)(b + i) * P + pidx];
-    }
-    for (; b < nblk; b++) acc[0] += gpart[(size_t)b * P + pidx];
-    float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    float s = 0.0f;
+#pragma unroll 4
+    for (int r = 0; r < rg; r++) s += tmp[(size_t)r * P + pidx];
     if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
     grad[pidx] = s;
   }
@@ -715,8 +882,9 @@ int launched(const char* what) {
   }
   return ACKPPO_OK;
 }
-constexpr size_t GRAD_LDS = (size_t)T_TOTAL * sizeof(float);
+constexpr size_t GRAD_LDS = (size_t)G_TOTAL * sizeof(float);
 bool g_grad_attr = false;
+float* g_reduce_tmp = nullptr;  // [REDUCE_RG][NPARAM] row-group sums (one small scratch per process)
 bool g_policy_attr = false;
 bool policy_lds_ready() {
   if (g_policy_attr) return true;
@@ -733,6 +901,11 @@ bool policy_lds_ready() {
 extern "C" {
 
 const char* ackppo_last_error(void) { return g_err; }
+#ifdef PP_STAMPS
+int ackppo_diag_set_stamps(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env_offset, uint64_t seed, uint32_t step,
                int deterministic, float* obs_rows, float* action, float* env_action, float* log_prob, float* value,
@@ -799,20 +972,31 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
   if (!g_grad_attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)ackppo_grad_kernel,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS);
-    if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the 159 KiB LDS tile");
+    if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the 158 KiB LDS footprint");
     g_grad_attr = true;
   }
   GradArgs A{params, obs_rows, actions, old_log_prob, advantages, returns, idx, batch, stats, clip_range, ent_coef,
              vf_coef, grad_partial, loss_partial};
-  hipLaunchKernelGGL(ackppo_grad_kernel, dim3((batch + TILE - 1) / TILE), dim3(GRAD_THREADS), GRAD_LDS,
+  hipLaunchKernelGGL(ackppo_grad_kernel, dim3(ackppo_grad_blocks(batch)), dim3(GRAD_THREADS), GRAD_LDS,
                      (hipStream_t)stream, A);
   return launched("ackppo_grad");
+}
+
+int ackppo_grad_blocks(int batch) {
+  if (batch <= 0) return 0;
+  const int tiles = (batch + GT - 1) / GT;
+  return tiles < GRAD_MAX_BLOCKS ? tiles : GRAD_MAX_BLOCKS;
 }
 
 int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream) {
   if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0) return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments");
-  hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, grad_partial,
+  const int rg = nblk < REDUCE_RG ? nblk : REDUCE_RG;
+  if (!g_reduce_tmp && hipMalloc(&g_reduce_tmp, sizeof(float) * P * REDUCE_RG) != hipSuccess)
+    return fail(ACKPPO_EHIP, "ackppo_reduce: scratch allocation");
+  hipLaunchKernelGGL(ackppo_reduce_rows_kernel, dim3((P + 255) / 256, rg), dim3(256), 0, (hipStream_t)stream,
+                     grad_partial, nblk, g_reduce_tmp);
+  hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, g_reduce_tmp, rg,
                      loss_partial, nblk, ent_coef, grad, loss);
   return launched("ackppo_reduce");
 }

@@ -31,7 +31,7 @@ import torch
 from .. import _lib, shard
 
 NOBS, NACT, HID = 79, 2, 64
-NPARAM, TILE, NLOSS = 18764, 64, 8
+NPARAM, NLOSS = 18764, 8
 # flat parameter layout = include/ackppo.h ACKPPO_OFF_* (policy.pth key names)
 LAYOUT = collections.OrderedDict([
     ("log_std", (0, (2,))),
@@ -143,7 +143,7 @@ class PPO:
         self.env_action = torch.zeros(N, NACT, **f32)
         self.last_dones = torch.ones(N, **f32)  # SB3 _last_episode_starts = ones at the first rollout
         self.last_values = torch.zeros(N, **f32)
-        nblk = (batch_size + TILE - 1) // TILE
+        nblk = self.L.ackppo_grad_blocks(batch_size)
         self.gpart = torch.zeros(nblk, NPARAM, **f32)  # pad words are never written: zero once
         self.lpart = torch.zeros(nblk, NLOSS, **f32)
         self.grad = torch.zeros(NPARAM, **f32)
@@ -240,7 +240,7 @@ class PPO:
                                              _ptr(self.buf_logp), _ptr(self.buf_adv), _ptr(self.buf_ret), _ptr(idx),
                                              nb, _ptr(self.mb_stats[m]), self.clip_range, self.ent_coef, self.vf_coef,
                                              _ptr(self.gpart), _ptr(self.lpart), s), "ackppo_grad")
-                _lib.ppo_check(L.ackppo_reduce(_ptr(self.gpart), _ptr(self.lpart), (nb + TILE - 1) // TILE,
+                _lib.ppo_check(L.ackppo_reduce(_ptr(self.gpart), _ptr(self.lpart), L.ackppo_grad_blocks(nb),
                                                self.ent_coef, _ptr(self.grad), _ptr(self.loss), s), "ackppo_reduce")
                 shard.all_reduce_sum_(self.grad, self.world)
                 self.adam_step += 1

@@ -123,7 +123,7 @@ def test_minibatch_gradient_and_adam_match_oracle(batch, ent_coef):
     t = lambda a: torch.tensor(a, device=DEV)
     stats = torch.zeros(1, 2, device=DEV)
     assert L().ackppo_adv_stats(P(t(adv)), P(t(idx)), batch, batch, 1, P(stats), S()) == 0
-    nblk = (batch + 63) // 64
+    nblk = L().ackppo_grad_blocks(batch)
     gpart, lpart = torch.zeros(nblk, po.NPARAM, device=DEV), torch.zeros(nblk, 8, device=DEV)
     grad, loss = torch.zeros(po.NPARAM, device=DEV), torch.zeros(8, device=DEV)
     assert L().ackppo_grad(P(p), P(t(obs)), P(t(acts)), P(t(old)), P(t(adv)), P(t(ret)), P(t(idx)), batch, P(stats),

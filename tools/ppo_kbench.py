@@ -31,7 +31,8 @@ def run(path):
     ret = torch.randn(S, device=dev)
     idx = torch.randperm(S, device=dev).to(torch.int32)
     stats = torch.tensor([0.0, 1.0], device=dev)
-    nblk = B // 64
+    L.ackppo_grad_blocks.argtypes = [i32]
+    nblk = L.ackppo_grad_blocks(B)
     gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
     grad, loss = torch.zeros(NP, device=dev), torch.zeros(8, device=dev)
     m, v, nrm = torch.zeros(NP, device=dev), torch.zeros(NP, device=dev), torch.zeros(1, device=dev)
@@ -61,5 +62,39 @@ def run(path):
     print(path, res, "grad checksum", float(grad.abs().sum()), flush=True)
 
 
-for p in sys.argv[1:]:
-    run(p)
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "--stamps"):
+    for p in sys.argv[1:]:
+        run(p)
+
+
+def stamps(path):
+    """Per-phase cycles of ackppo_grad from the PP_STAMPS build (median over workgroups)."""
+    L = C.CDLL(path)
+    p32, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    L.ackppo_grad.argtypes = [p32] * 7 + [i32, p32, f32, f32, f32, p32, p32, p32]
+    L.ackppo_diag_set_stamps.argtypes = [p32]
+    S, B = 131072, 8192
+    params = (torch.randn(NP) * 0.1).to(dev)
+    obs, act = torch.randn(S, 79, device=dev), torch.randn(S, 2, device=dev)
+    lp, adv, ret = torch.randn(S, device=dev), torch.randn(S, device=dev), torch.randn(S, device=dev)
+    idx = torch.randperm(S, device=dev).to(torch.int32)
+    stats = torch.tensor([0.0, 1.0], device=dev)
+    L.ackppo_grad_blocks.argtypes = [C.c_int]
+    nblk = L.ackppo_grad_blocks(B)
+    gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
+    st = torch.zeros(16 * nblk, dtype=torch.int64, device=dev)
+    L.ackppo_diag_set_stamps(P(st))
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        L.ackppo_grad(P(params), P(obs), P(act), P(lp), P(adv), P(ret), P(idx), B, P(stats), 0.2, 0.0, 0.5, P(gp),
+                      P(lpart), s)
+    torch.cuda.synchronize()
+    a = st.cpu().numpy().reshape(16, nblk)
+    used = [k for k in range(16) if a[k].any()]
+    print("grad phases (median cycles per workgroup):",
+          {f"{used[i]}->{used[i + 1]}": int(np.median(a[used[i + 1]] - a[used[i]])) for i in range(len(used) - 1)},
+          "total", int(np.median(a[used[-1]] - a[used[0]])))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--stamps":
+    stamps(sys.argv[2])
