@@ -21,7 +21,12 @@ PHASES = [(0, 1, "controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3, 4, 
           (11, 12, "rays"), (12, 9, "obs stores+reward"), (9, 10, "state store")]
 
 
+QUAD_PHASES = [(0, 5, "pre-newton"), (5, 6, "newton"), (6, 10, "post-newton")]
+
+
 def main():
+    quad = len(sys.argv) > 1 and sys.argv[1] == "quad"
+    phases = QUAD_PHASES if quad else PHASES
     L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", "libackphys_stamps.so"))
     P = C.c_void_p
     L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
@@ -35,13 +40,13 @@ def main():
     ctx = P()
     assert L.ackphys_create(blob, len(blob), n, 0, C.byref(ctx)) == 0
     L.ackphys_set_variant.argtypes = [P, C.c_int]
-    assert L.ackphys_set_variant(ctx, 0) == 0  # stamps are in the lane-per-env kernel
+    assert L.ackphys_set_variant(ctx, 1 if quad else 0) == 0
     state = torch.zeros(44, n, device=dev)
     obs = torch.zeros(79, n, device=dev)
     rew = torch.zeros(n, device=dev)
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nb = (n + 63) // 64
+    nb = (n + 15) // 16 if quad else (n + 63) // 64
     stamps = torch.zeros(16 * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
     p = lambda t: P(t.data_ptr())
@@ -63,23 +68,25 @@ def main():
             torch.cuda.synchronize()
             allv = stamps.cpu().numpy()
             s = allv[: 16 * nb].reshape(16, nb)
-            res.append(np.stack([s[b] - s[a] for a, b, _ in PHASES]))
+            res.append(np.stack([s[b] - s[a] for a, b, _ in phases]))
             its = allv[16 * nb:16 * nb + 64 * nb]
             nt = allv[16 * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
                 print("  newton phases (median cycles/wave, summed over iterations): " + ", ".join(
                     f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"])))
             its = its[: 64 * nb]
+            if quad:
+                its = its.reshape(nb, 64)[:, :16].reshape(-1)
             if k == 200:
                 itn, why = its // 8, its % 8
-                wmax = itn.reshape(nb, 64).max(axis=1)
+                wmax = itn.reshape(nb, -1).max(axis=1)
                 print(f"  iterations: lane mean {itn.mean():.2f}, lane hist {np.bincount(itn, minlength=13)}, "
                       f"wave-max hist {np.bincount(wmax, minlength=13)}, exit reasons (1 exact,2 grad,3 nodesc,4 maxit) "
                       f"{np.bincount(why, minlength=5)[1:]}")
         d = np.median(np.concatenate(res, axis=1), axis=1)
         tot = np.median(np.concatenate([np.sum(r, axis=0) for r in res]))
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
-        for (_, _, name), v in zip(PHASES, d):
+        for (_, _, name), v in zip(phases, d):
             print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
 
 

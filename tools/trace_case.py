@@ -8,8 +8,13 @@ import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-d = np.load(os.path.join(REPO, "tests", "golden", "slow_newton_cases.npz"))
-idxs = [int(x) for x in sys.argv[1:]] or list(np.argsort(-d["it"])[:3])
+args = sys.argv[1:]
+flags = 2
+if args and args[0] == "--contacts":
+    flags, args = 3, args[1:]
+d = np.load(os.path.join(REPO, "tests", "golden",
+                         "slow_newton_cases_contacts.npz" if flags & 1 else "slow_newton_cases.npz"))
+idxs = [int(x) for x in args] or list(np.argsort(-d["it"])[:3])
 L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", "libackphys_trace.so"))
 P = C.c_void_p
 L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
@@ -27,6 +32,6 @@ for i in idxs:
     act = torch.tensor(d["action"][i][None].copy(), device=dev)
     obs, rew = torch.zeros(79, 1, device=dev), torch.zeros(1, device=dev)
     term, trunc = torch.zeros(1, dtype=torch.uint8, device=dev), torch.zeros(1, dtype=torch.uint8, device=dev)
-    L.ackphys_step(ctx, p(act), p(st), p(obs), p(rew), p(term), p(trunc), None, None, None, 2, 0,
+    L.ackphys_step(ctx, p(act), p(st), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
                    P(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
