@@ -1,0 +1,90 @@
+"""PPO training run on the batched env (configs[3]/[4]-style "PPO rollout to convergence" on
+the flat scene): learning curve + deterministic goal-reach evaluation -> one JSON line per
+evaluation.
+
+    python tools/train_ppo.py [--envs 4096] [--iters 400] [--eval-every 25] [--out gpurun_out/train_ppo.jsonl]
+
+Env: make_ackermann_env(env_type="vec") defaults (the reference's make_env signature:
+max_linear_velocity 0.5, goal_distance_threshold 0.3), contacts on. PPO: SB3 semantics
+(rl/ppo.py) with n_steps 32, batch 8192, 10 epochs, lr 3e-4 for 4096 envs.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mujoco_playground_amd.rl import make_ackermann_env  # noqa: E402
+from mujoco_playground_amd.rl.ppo import PPO  # noqa: E402
+
+
+def evaluate(model, n=1024, horizon=1000, seed=123, **env_kw):
+    """Deterministic policy from fresh resets: fraction of envs that reach their goal within the
+    horizon, and the mean steps to the goal for those that do."""
+    env = make_ackermann_env(env_type="vec", num_envs=n, device=model.device, seed=seed,
+                             max_episode_steps=horizon + 1, **env_kw)
+    sim = env.sim
+    env.reset()
+    done = torch.zeros(n, dtype=torch.bool, device=model.device)
+    t_goal = torch.full((n,), float(horizon), device=model.device)
+    for t in range(horizon):
+        a, _ = model.predict(sim.obs_soa.t(), deterministic=True)
+        sim.step(a, autoreset=False, want_info=False, want_terminal=False, track_episodes=False)
+        hit = sim.term.bool() & ~done
+        t_goal[hit] = float(t + 1)
+        done |= hit
+        if t % 50 == 49 and bool(done.all()):
+            break
+    succ = float(done.float().mean())
+    return succ, float(t_goal[done].mean()) if bool(done.any()) else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--iters", type=int, default=400)
+    ap.add_argument("--eval-every", type=int, default=25)
+    ap.add_argument("--out", default="gpurun_out/train_ppo.jsonl")
+    ap.add_argument("--collision-threshold", type=float, default=0.15,
+                    help="0.15 = the reference (a -1 'no hit' lidar reading counts as a collision, so on the "
+                         "open floor every step costs -50); < -1 removes that term")
+    ap.add_argument("--max-episode-steps", type=int, default=1000,
+                    help="1000 = the reference (2 s of sim time: at <= 0.5 m/s the 2-8 m goals are out of reach)")
+    ap.add_argument("--gamma", type=float, default=0.99)
+    ap.add_argument("--ent-coef", type=float, default=0.0)
+    ap.add_argument("--n-steps", type=int, default=32)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    env_kw = dict(collision_threshold=a.collision_threshold)
+    horizon = a.max_episode_steps
+    venv = make_ackermann_env(env_type="vec", num_envs=a.envs, device=dev, seed=0,
+                              max_episode_steps=a.max_episode_steps, **env_kw)
+    model = PPO("MlpPolicy", venv, n_steps=a.n_steps, batch_size=8192, n_epochs=10, learning_rate=3e-4,
+                ent_coef=a.ent_coef, gamma=a.gamma, seed=0)
+    out = open(a.out, "w")
+    t0 = time.perf_counter()
+    succ, tg = evaluate(model, horizon=horizon, **env_kw)
+    rec = {"iter": 0, "env_steps": 0, "wall_s": 0.0, "eval_success": succ, "eval_steps_to_goal": tg}
+    print(json.dumps(rec), flush=True)
+    out.write(json.dumps(rec) + "\n")
+    for it in range(1, a.iters + 1):
+        model.learn(total_timesteps=model.n_steps * a.envs)  # one rollout + update per call
+        if it % a.eval_every == 0 or it == a.iters:
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            succ, tg = evaluate(model, horizon=horizon, **env_kw)
+            lg = model.logger
+            rec = {"iter": it, "env_steps": it * model.n_steps * a.envs, "wall_s": round(wall, 2),
+                   "ep_rew_mean": lg.get("rollout/ep_rew_mean"), "episodes": lg.get("rollout/episodes_total"),
+                   "value_loss": lg.get("train/value_loss"), "approx_kl": lg.get("train/approx_kl"),
+                   "std": lg.get("train/std"), "eval_success": succ, "eval_steps_to_goal": tg}
+            print(json.dumps(rec), flush=True)
+            out.write(json.dumps(rec) + "\n")
+            out.flush()
+
+
+if __name__ == "__main__":
+    main()
