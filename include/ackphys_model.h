@@ -15,9 +15,9 @@
 #include <stdint.h>
 
 #define APM_MAGIC 0x4D504841u /* "AHPM" */
-#define APM_VERSION 1u
+#define APM_VERSION 2u
 
-#define APM_MAXBODY 48
+#define APM_MAXBODY 64
 #define APM_MAXJNT 8
 #define APM_MAXQ 16
 #define APM_MAXDOF 16
@@ -106,6 +106,10 @@ typedef struct apm_model {
   int32_t mesh_faceadr[APM_MAXMESH], mesh_facenum[APM_MAXMESH];
   int32_t mesh_hulladr[APM_MAXMESH], mesh_hullnum[APM_MAXMESH];
   double mesh_aabb[APM_MAXMESH][6]; /* centre[3], half-size[3] in the mesh (geom) frame */
+
+  /* env spawn point written into the free joint by the reset (scene property; v2: 0 0 0.1,
+     simple_map_spawner.py:43) */
+  double spawn[3];
 } apm_model_t;
 
 /* Trailing arrays, in order, each starting at hdr_bytes + running offset:

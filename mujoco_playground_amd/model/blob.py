@@ -15,9 +15,9 @@ import numpy as np
 from .compiler import CompiledModel
 
 APM_MAGIC = 0x4D504841
-APM_VERSION = 1
+APM_VERSION = 2
 MAXBODY, MAXJNT, MAXQ, MAXDOF, MAXGEOM, MAXSITE, MAXSENSOR, MAXU, MAXEQ, MAXMESH = (
-    48, 8, 16, 16, 64, 80, 96, 4, 2, 4)
+    64, 8, 16, 16, 64, 80, 96, 4, 2, 4)
 
 i32, f64, u32 = C.c_int32, C.c_double, C.c_uint32
 
@@ -83,6 +83,7 @@ class APMModel(C.Structure):
         ("mesh_faceadr", _a(i32, MAXMESH)), ("mesh_facenum", _a(i32, MAXMESH)),
         ("mesh_hulladr", _a(i32, MAXMESH)), ("mesh_hullnum", _a(i32, MAXMESH)),
         ("mesh_aabb", _a(f64, MAXMESH, 6)),
+        ("spawn", _a(f64, 3)),
     ]
 
 
@@ -108,6 +109,7 @@ def pack(m: CompiledModel) -> bytes:
     s.iterations, s.ls_iterations = m.iterations, m.ls_iterations
     s.timestep, s.tolerance, s.impratio, s.meaninertia = m.timestep, m.tolerance, m.impratio, m.meaninertia
     _put(s.gravity, m.gravity)
+    _put(s.spawn, m.spawn)
     for f in ["body_parentid", "body_rootid", "body_weldid", "body_jntadr", "body_jntnum",
               "body_dofadr", "body_dofnum", "body_pos", "body_quat", "body_ipos", "body_iquat",
               "body_mass", "body_inertia", "body_invweight0",

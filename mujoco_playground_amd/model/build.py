@@ -5,6 +5,8 @@
 Writes
   mujoco_playground_amd/model/assets/ackermann_robot_v2.apm   (blob for ackphys_create)
   mujoco_playground_amd/csrc/ackphys_model_gen.h              (constexpr kernel constants)
+  mujoco_playground_amd/model/assets/ackermann_obstacles.apm  (obstacle scene blob)
+  mujoco_playground_amd/csrc/ackphys_scene_gen.h              (its static-world constants)
 Both are committed: the GPU box has no /root/reference, so it only consumes them.
 """
 from __future__ import annotations
@@ -13,12 +15,14 @@ import argparse
 import os
 
 from . import blob as blobmod
-from .codegen import generate
-from .compiler import compile_mjcf, default_model_path
+from .codegen import generate, generate_scene
+from .compiler import compile_mjcf, compile_scene, default_model_path, obstacle_scene_path
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
 HEADER_PATH = os.path.join(PKG, "csrc", "ackphys_model_gen.h")
+SCENE_BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_obstacles.apm")
+SCENE_HEADER_PATH = os.path.join(PKG, "csrc", "ackphys_scene_gen.h")
 
 
 def build(reference_root: str = "/root/reference", check_only: bool = False) -> bool:
@@ -26,14 +30,16 @@ def build(reference_root: str = "/root/reference", check_only: bool = False) -> 
     m = compile_mjcf(default_model_path(reference_root))
     b = blobmod.pack(m)
     hdr = generate(m, blobmod.fnv1a64(b))
-    same = (os.path.exists(BLOB_PATH) and open(BLOB_PATH, "rb").read() == b
-            and os.path.exists(HEADER_PATH) and open(HEADER_PATH).read() == hdr)
+    ms = compile_scene(obstacle_scene_path(reference_root), default_model_path(reference_root))
+    bs = blobmod.pack(ms)
+    hs = generate_scene(ms, blobmod.fnv1a64(bs), m)
+    outs = [(BLOB_PATH, b), (HEADER_PATH, hdr.encode()), (SCENE_BLOB_PATH, bs), (SCENE_HEADER_PATH, hs.encode())]
+    same = all(os.path.exists(p) and open(p, "rb").read() == data for p, data in outs)
     if not same and not check_only:
-        os.makedirs(os.path.dirname(BLOB_PATH), exist_ok=True)
-        with open(BLOB_PATH, "wb") as f:
-            f.write(b)
-        with open(HEADER_PATH, "w") as f:
-            f.write(hdr)
+        for p, data in outs:
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "wb") as f:
+                f.write(data)
     return same
 
 

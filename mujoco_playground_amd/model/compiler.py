@@ -151,6 +151,8 @@ class CompiledModel:
     # meshes
     meshes: list = field(default_factory=list)
     mesh_inertia_mode: str = "legacy"
+    # env spawn point (x, y, z) the reset writes into the free joint (scene property, see merge_scene)
+    spawn: np.ndarray = field(default_factory=lambda: np.array([0.0, 0.0, 0.1]))
 
     @property
     def nbody(self):
@@ -296,6 +298,9 @@ def _parse_geom(ch, angle_scale):
         g["mass"] = float(g["mass"])
     fr = list(g["friction"]) + list(DEFAULT_FRICTION[len(g["friction"]):])
     g["friction"] = np.array(fr[:3])
+    # partially specified solref/solimp keep MuJoCo's defaults for the remaining entries
+    g["solref"] = np.array((list(g["solref"]) + list(DEFAULT_SOLREF[len(g["solref"]):]))[:2])
+    g["solimp"] = np.array((list(g["solimp"]) + list(DEFAULT_SOLIMP[len(g["solimp"]):]))[:5])
     sz = list(g["size"]) + [0.0] * (3 - len(g["size"]))
     g["size"] = np.array(sz[:3])
     return g
@@ -303,10 +308,31 @@ def _parse_geom(ch, angle_scale):
 
 # ----------------------------------------------------------------------------- compile
 
+def _apply_geom_defaults(root):
+    """Top-level `<default><geom .../></default>`: attributes a geom does not set itself are
+    taken from it (MJCF main default class; nested classes are not used by these models)."""
+    dflt = root.find("default")
+    if dflt is None:
+        return
+    for ch in dflt:
+        if ch.tag == "default":
+            raise NotImplementedError("nested default classes")
+        if ch.tag != "geom":
+            raise NotImplementedError(f"<default><{ch.tag}>")
+        for g in root.iter("geom"):
+            for k, v in ch.attrib.items():
+                if k not in g.attrib:
+                    g.set(k, v)
+
+
 def compile_mjcf(xml_path: str, mesh_inertia: str = "legacy") -> CompiledModel:
     xml_path = os.path.abspath(xml_path)
-    root = ET.parse(xml_path).getroot()
-    base = os.path.dirname(xml_path)
+    return compile_root(ET.parse(xml_path).getroot(), os.path.dirname(xml_path), mesh_inertia)
+
+
+def compile_root(root, base: str, mesh_inertia: str = "legacy", spawn=(0.0, 0.0, 0.1)) -> CompiledModel:
+    root = ET.fromstring(ET.tostring(root))   # private copy: defaults are applied in place
+    _apply_geom_defaults(root)
     angle_scale = np.pi / 180.0
     comp = root.find("compiler")
     if comp is not None and comp.get("angle", "degree") == "radian":
@@ -318,7 +344,7 @@ def compile_mjcf(xml_path: str, mesh_inertia: str = "legacy") -> CompiledModel:
     mesh_files = {}
     for asset in root.findall("asset"):
         for m in asset.findall("mesh"):
-            mesh_files[m.get("name")] = os.path.join(base, m.get("file"))
+            mesh_files[m.get("name")] = os.path.join(base, m.get("file"))   # absolute paths pass through
     meshes, mesh_id = [], {}
     for name, path in mesh_files.items():
         mesh_id[name] = len(meshes)
@@ -339,6 +365,7 @@ def compile_mjcf(xml_path: str, mesh_inertia: str = "legacy") -> CompiledModel:
 
     # MuJoCo body order is depth-first pre-order, which is the order _parse_body appends.
     m = CompiledModel(name=root.get("model", "model"), timestep=timestep, gravity=gravity)
+    m.spawn = np.array(spawn, dtype=np.float64)
     m.meshes = meshes
     m.mesh_inertia_mode = mesh_inertia
     nb = len(bodies)
@@ -464,6 +491,8 @@ def compile_mjcf(xml_path: str, mesh_inertia: str = "legacy") -> CompiledModel:
         gs = [(k, g) for k, (bb, g) in enumerate(gl) if bb == i]
         if not gs:
             continue
+        if weldid[i] == 0:
+            continue   # static body (welded to the world): its inertia never enters the dynamics
         if len(gs) != 1:
             raise NotImplementedError("multi-geom inertia inference")
         k, g = gs[0]
@@ -662,3 +691,92 @@ def _set_const(m: CompiledModel):
 
 def default_model_path(reference_root: str = "/root/reference") -> str:
     return os.path.join(reference_root, "models", "ackermann_robot_v2.xml")
+
+
+def obstacle_scene_path(reference_root: str = "/root/reference") -> str:
+    return os.path.join(reference_root, "models", "environments", "ackermann_maze_flat.xml")
+
+
+# ----------------------------------------------------------------------------- scene merge
+
+def merge_scene(scene_xml: str, robot_xml: str):
+    """The obstacle scene: the v2 robot merged into a static world.
+
+    The merge follows the reference's robot-into-maze rules
+    (src/rl/envs/ackermann_gymnasium_maze_env.py:237-398):
+      * the robot's <compiler> attributes override the scene's (:249-258), the robot's
+        option gravity/timestep override the scene's (:262-271);
+      * robot assets are added (:298-311) -- the robot's mesh files are used for the shared
+        mesh names, because the scene file's own paths (`../CAD Models/` relative to
+        models/environments/) point at a directory the reference does not have;
+      * the robot's chassis subtree, sensors, actuators and equality constraints are appended
+        (:354-398).
+    Scene-specific choices (documented in DESIGN.md §11):
+      * the scene file's OWN robot (its free-joint `chassis` body and the sensors/actuators that
+        reference it; it has torque drives and 36 lidar sites, which the v2 controller and
+        observation code cannot drive) is removed, and its chassis position becomes the env
+        spawn point (x, y) -- the reference's spawn (0, 0) lies inside obstacle_22 here;
+      * the maze rule that lowers geoms named *floor* to z = -0.5 and lifts *block* geoms
+        (:322-352) is for gymnasium-robotics mazes; the flat scene's obstacles are named
+        obstacle_*, so applying it would leave them hovering -- the scene geometry is kept;
+      * the scene's top-level <default> applies to every geom of the merged file (MJCF
+        semantics), so robot, floor and obstacle contacts all use its solref/solimp.
+    Returns (root Element, base directory, spawn xyz).
+    """
+    scene = ET.parse(scene_xml).getroot()
+    robot = ET.parse(robot_xml).getroot()
+    rc, sc = robot.find("compiler"), scene.find("compiler")
+    if rc is not None:
+        if sc is None:
+            sc = ET.SubElement(scene, "compiler")
+        for k, v in rc.attrib.items():
+            sc.set(k, v)
+    ro, so = robot.find("option"), scene.find("option")
+    if ro is not None:
+        if so is None:
+            so = ET.SubElement(scene, "option")
+        for k in ("gravity", "timestep"):
+            if k in ro.attrib:
+                so.set(k, ro.get(k))
+    rbase = os.path.dirname(os.path.abspath(robot_xml))
+    sassets = scene.findall("asset")
+    if not sassets:
+        sassets = [ET.SubElement(scene, "asset")]
+    for ra in robot.findall("asset"):
+        for item in ra:
+            item = ET.fromstring(ET.tostring(item))
+            if "file" in item.attrib and not os.path.isabs(item.get("file")):
+                item.set("file", os.path.normpath(os.path.join(rbase, item.get("file"))))
+            for a in sassets:
+                for old in list(a):
+                    if old.tag == item.tag and old.get("name") == item.get("name"):
+                        a.remove(old)
+            sassets[0].append(item)
+    swb, rwb = scene.find("worldbody"), robot.find("worldbody")
+    spawn = None
+    for b in list(swb):
+        if b.tag == "body" and (b.find("freejoint") is not None or b.find("joint") is not None):
+            if spawn is not None:
+                raise NotImplementedError("more than one free body in the scene")
+            p = _floats(b.get("pos", "0 0 0"), 3)
+            spawn = (p[0], p[1], 0.1)   # reset height of AckermannRobotEnv.reset (robot_pos z = 0.1)
+            swb.remove(b)
+    if spawn is None:
+        spawn = (0.0, 0.0, 0.1)
+    for tag in ("sensor", "actuator", "equality"):
+        for el in scene.findall(tag):
+            scene.remove(el)
+    chassis = rwb.find("body[@name='chassis']")
+    swb.append(ET.fromstring(ET.tostring(chassis)))
+    for tag in ("sensor", "actuator", "equality"):
+        el = robot.find(tag)
+        if el is not None:
+            scene.append(ET.fromstring(ET.tostring(el)))
+    return scene, os.path.dirname(os.path.abspath(scene_xml)), spawn
+
+
+def compile_scene(scene_xml: str, robot_xml: str, mesh_inertia: str = "legacy") -> CompiledModel:
+    root, base, spawn = merge_scene(scene_xml, robot_xml)
+    m = compile_root(root, base, mesh_inertia, spawn)
+    m.name = root.get("model", "scene")
+    return m

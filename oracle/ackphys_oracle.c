@@ -60,8 +60,17 @@
 #define CTL_WHEELBASE 0.20
 #define CTL_TRACK 0.174
 
+#define OR_MAXFEAT 96
+/* convex-hull features (geom frame) for the box-convex separating-axis test */
+typedef struct {
+  int nf, ne;
+  double fn[OR_MAXFEAT][3]; /* unique outward face normals */
+  double ed[OR_MAXFEAT][3]; /* unique edge directions (up to sign) */
+} or_hullfeat;
+
 struct or_ctx {
   const apm_model_t* m;
+  or_hullfeat hf[APM_MAXMESH];
   const float* mesh_vert;
   const int32_t* mesh_face;
   const float* hull_vert;
@@ -245,8 +254,77 @@ void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
 }
 static double u01(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
 
-/* ------------------------------------------------------------------ model setup */
+/* ------------------------------------------------------------------ convex hull features
+   Faces = supporting planes through 3 hull vertices (all vertices on one side); edges = vertex
+   pairs lying on >= 2 distinct face planes. Brute force, once per context (36 vertices here). */
+static void feat_add(double (*arr)[3], int* n, const double v[3], int sign_free) {
+  for (int i = 0; i < *n; i++) {
+    double dd = dot3(arr[i], v);
+    if (dd > 1 - 1e-9 || (sign_free && dd < -1 + 1e-9)) return;
+  }
+  if (*n < OR_MAXFEAT) { memcpy(arr[*n], v, sizeof(double) * 3); (*n)++; }
+}
+static void hull_features(const float* hv, int n, or_hullfeat* f) {
+  f->nf = f->ne = 0;
+  double scale = 0;
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < 3; k++) scale = fmax(scale, fabs((double)hv[3 * i + k]));
+  const double tol = 1e-9 * (scale > 0 ? scale : 1);
+#define HV(i, k) ((double)hv[3 * (i) + (k)])
+  for (int i = 0; i < n; i++)
+    for (int j = i + 1; j < n; j++)
+      for (int k = j + 1; k < n; k++) {
+        double e1[3] = {HV(j, 0) - HV(i, 0), HV(j, 1) - HV(i, 1), HV(j, 2) - HV(i, 2)};
+        double e2[3] = {HV(k, 0) - HV(i, 0), HV(k, 1) - HV(i, 1), HV(k, 2) - HV(i, 2)};
+        double nn[3];
+        cross3(nn, e1, e2);
+        double len = sqrt(dot3(nn, nn));
+        if (len < 1e-12 * scale * scale) continue;
+        for (int t = 0; t < 3; t++) nn[t] /= len;
+        double off = nn[0] * HV(i, 0) + nn[1] * HV(i, 1) + nn[2] * HV(i, 2);
+        int above = 0, below = 0;
+        for (int v = 0; v < n; v++) {
+          double sd = nn[0] * HV(v, 0) + nn[1] * HV(v, 1) + nn[2] * HV(v, 2) - off;
+          if (sd > tol) above++;
+          else if (sd < -tol) below++;
+        }
+        if (above && below) continue;
+        if (above) for (int t = 0; t < 3; t++) nn[t] = -nn[t];
+        feat_add(f->fn, &f->nf, nn, 0);
+      }
+  double off[OR_MAXFEAT];
+  for (int a = 0; a < f->nf; a++) {
+    off[a] = -1e300;
+    for (int v = 0; v < n; v++) off[a] = fmax(off[a], f->fn[a][0] * HV(v, 0) + f->fn[a][1] * HV(v, 1) + f->fn[a][2] * HV(v, 2));
+  }
+  for (int i = 0; i < n; i++)
+    for (int j = i + 1; j < n; j++) {
+      double e[3] = {HV(j, 0) - HV(i, 0), HV(j, 1) - HV(i, 1), HV(j, 2) - HV(i, 2)};
+      double len = sqrt(dot3(e, e));
+      if (len < tol) continue;
+      int on = 0;
+      for (int a = 0; a < f->nf; a++) {
+        double si = f->fn[a][0] * HV(i, 0) + f->fn[a][1] * HV(i, 1) + f->fn[a][2] * HV(i, 2) - off[a];
+        double sj = f->fn[a][0] * HV(j, 0) + f->fn[a][1] * HV(j, 1) + f->fn[a][2] * HV(j, 2) - off[a];
+        if (fabs(si) < tol && fabs(sj) < tol) on++;
+      }
+      if (on < 2) continue;
+      for (int t = 0; t < 3; t++) e[t] /= len;
+      feat_add(f->ed, &f->ne, e, 1);
+    }
+#undef HV
+}
+int or_hull_features(const or_ctx* c, int mesh, double* fn, double* ed, int* nf, int* ne) {
+  if (mesh < 0 || mesh >= c->m->nmesh) return -1;
+  const or_hullfeat* f = &c->hf[mesh];
+  memcpy(fn, f->fn, sizeof(double) * 3 * f->nf);
+  memcpy(ed, f->ed, sizeof(double) * 3 * f->ne);
+  *nf = f->nf;
+  *ne = f->ne;
+  return 0;
+}
 
+/* ------------------------------------------------------------------ model setup */
 static int find_actuator(const apm_model_t* m, int jnt) {
   for (int i = 0; i < m->nu; i++)
     if (m->actuator_trnid[i] == jnt) return i;
@@ -266,9 +344,11 @@ int or_create(const void* blob, size_t nbytes, or_ctx** out) {
   c->mesh_vert = (const float*)tail;
   c->mesh_face = (const int32_t*)(tail + 12 * (size_t)c->m->nmeshvert);
   c->hull_vert = (const float*)(tail + 12 * (size_t)c->m->nmeshvert + 12 * (size_t)c->m->nmeshface);
+  for (int k = 0; k < c->m->nmesh; k++)
+    hull_features(c->hull_vert + 3 * c->m->mesh_hulladr[k], c->m->mesh_hullnum[k], &c->hf[k]);
   c->tolerance = 1e-12; /* tighter than MuJoCo's 1e-8: the oracle targets the exact optimum */
   c->maxiter = c->m->iterations;
-  c->chassis_body = 1;
+  c->chassis_body = c->m->jnt_bodyid[0]; /* the free joint's body ("chassis") */
   c->max_steps = 1000; c->goal_thresh = 0.5; c->coll_thresh = 0.15; c->max_lin = 1.0; c->max_ang = 1.0;
   /* BicycleController actuator lookup by name (controller.py:94-96): steering servo on the
      first limited hinge, rear drives on the first two hinges -- resolved by trnid order. */
@@ -689,6 +769,181 @@ static int plane_convex(const or_ctx* c, const or_data* d, int g1, int g2, doubl
   return nsel;
 }
 
+/* ---------------- box vs convex geoms (obstacle scene)
+   MuJoCo routes box-cylinder and box-mesh pairs to its general convex collider, which returns
+   ONE contact per pair (multiccd off) at its estimate of the minimum translation [ext]. This
+   restatement computes that minimum translation by a separating-axis test over a fixed
+   candidate set with exact support functions:
+     box-mesh:     box axes, hull face normals, hull edge dirs x box axes (complete for polytopes);
+     cylinder-box: box axes, cylinder axis, cylinder axis x box axes, and for each box axis
+                   whose edges come within the cylinder's bounding radius, the best direction
+                   perpendicular to that axis (edge-rim contacts; 1-D search, see edge_family).
+   dist = the largest separation over the set (<= 0: penetration), normal from geom1 to geom2
+   (MuJoCo pair order: cylinder(5) < box(6) < mesh(7)); the contact point is the robot geom's
+   deepest point moved half the penetration back (the witness midpoint). Support points that are
+   not unique (face/edge parallel to the separating plane) average the candidates within 1 um. */
+#define OR_TIE 1e-6
+static void box_frame(const or_data* d, const apm_model_t* m, int g, double c[3], double A[3][3], double h[3]) {
+  for (int k = 0; k < 3; k++) {
+    c[k] = d->geom_xpos[g][k];
+    h[k] = m->geom_size[g][k];
+    for (int t = 0; t < 3; t++) A[k][t] = d->geom_xmat[g][3 * t + k]; /* A[k] = k-th box axis (world) */
+  }
+}
+static double box_radius(const double A[3][3], const double h[3], const double n[3]) {
+  return h[0] * fabs(dot3(A[0], n)) + h[1] * fabs(dot3(A[1], n)) + h[2] * fabs(dot3(A[2], n));
+}
+/* separation of geom2's interval [lo2, hi2] from geom1's [lo1, hi1] along +-n; keeps the best */
+static int sat_axis(const double n[3], double lo1, double hi1, double lo2, double hi2, double* best, double nb[3]) {
+  double s1 = lo2 - hi1, s2 = lo1 - hi2;
+  double sep = s1 >= s2 ? s1 : s2;
+  if (sep > *best) {
+    *best = sep;
+    double sg = s1 >= s2 ? 1.0 : -1.0;
+    nb[0] = sg * n[0]; nb[1] = sg * n[1]; nb[2] = sg * n[2];
+  }
+  return sep > 0;
+}
+static double cyl_extent(const double a[3], double r, double h, const double n[3]) {
+  double an = dot3(a, n);
+  return h * fabs(an) + r * sqrt(fmax(0.0, 1.0 - an * an));
+}
+/* box (geom1) vs convex mesh (geom2) */
+static int box_convex(const or_ctx* c, const or_data* d, int gb, int gm, or_contact* con) {
+  const apm_model_t* m = c->m;
+  double bc[3], A[3][3], bh[3];
+  box_frame(d, m, gb, bc, A, bh);
+  int mid = m->geom_dataid[gm];
+  const float* hv = c->hull_vert + 3 * m->mesh_hulladr[mid];
+  int nh = m->mesh_hullnum[mid];
+  const double* R = d->geom_xmat[gm];
+  double w[64][3];
+  for (int i = 0; i < nh && i < 64; i++) {
+    double v[3] = {hv[3 * i], hv[3 * i + 1], hv[3 * i + 2]};
+    mulmatvec3(w[i], R, v);
+    for (int k = 0; k < 3; k++) w[i][k] += d->geom_xpos[gm][k];
+  }
+  const or_hullfeat* f = &c->hf[mid];
+  double best = -1e300, nb[3] = {0, 0, 1};
+  int nax = 3 + f->nf + 3 * f->ne;
+  for (int a = 0; a < nax; a++) {
+    double n[3];
+    if (a < 3) { memcpy(n, A[a], sizeof n); }
+    else if (a < 3 + f->nf) { mulmatvec3(n, R, f->fn[a - 3]); }
+    else {
+      int e = (a - 3 - f->nf) / 3, k = (a - 3 - f->nf) % 3;
+      double ew[3];
+      mulmatvec3(ew, R, f->ed[e]);
+      cross3(n, ew, A[k]);
+      double len = sqrt(dot3(n, n));
+      if (len < 1e-6) continue;
+      for (int t = 0; t < 3; t++) n[t] /= len;
+    }
+    double lo = 1e300, hi = -1e300;
+    for (int i = 0; i < nh; i++) {
+      double pr = dot3(w[i], n);
+      lo = fmin(lo, pr);
+      hi = fmax(hi, pr);
+    }
+    double cb = dot3(bc, n), rb = box_radius(A, bh, n);
+    if (sat_axis(n, cb - rb, cb + rb, lo, hi, &best, nb)) return 0;
+  }
+  /* witness: the hull's deepest point into the box (support along -nb), ties averaged */
+  double mn = 1e300;
+  for (int i = 0; i < nh; i++) mn = fmin(mn, dot3(w[i], nb));
+  double wp[3] = {0, 0, 0};
+  int cnt = 0;
+  for (int i = 0; i < nh; i++)
+    if (dot3(w[i], nb) <= mn + OR_TIE) { for (int k = 0; k < 3; k++) wp[k] += w[i][k]; cnt++; }
+  con->dist = best;
+  for (int k = 0; k < 3; k++) con->pos[k] = wp[k] / cnt - 0.5 * best * nb[k];
+  memcpy(con->frame, nb, sizeof nb);
+  return 1;
+}
+/* cylinder (geom1) vs box (geom2) */
+static double cyl_box_sep(const double cc[3], const double a[3], double r, double h, const double bc[3],
+                          const double A[3][3], const double bh[3], const double n[3], double* sgn) {
+  double cn = dot3(cc, n), ce = cyl_extent(a, r, h, n);
+  double cb = dot3(bc, n), rb = box_radius(A, bh, n);
+  double s1 = (cb - rb) - (cn + ce), s2 = (cn - ce) - (cb + rb);
+  *sgn = s1 >= s2 ? 1.0 : -1.0;
+  return s1 >= s2 ? s1 : s2;
+}
+/* separation maximised over the directions perpendicular to box axis k (box-edge vs cap-rim
+   contacts): 32 samples of the half circle, then 24 ternary-search rounds around the best */
+static void edge_family(const double cc[3], const double a[3], double r, double h, const double bc[3],
+                        const double A[3][3], const double bh[3], int k, double n_out[3]) {
+  const double* u = A[(k + 1) % 3];
+  const double* w = A[(k + 2) % 3];
+  double sg, bestv = -1e300, bphi = 0;
+  for (int i = 0; i < 32; i++) {
+    double phi = M_PI * i / 32.0, n[3];
+    for (int t = 0; t < 3; t++) n[t] = cos(phi) * u[t] + sin(phi) * w[t];
+    double v = cyl_box_sep(cc, a, r, h, bc, A, bh, n, &sg);
+    if (v > bestv) { bestv = v; bphi = phi; }
+  }
+  double lo = bphi - M_PI / 32.0, hi = bphi + M_PI / 32.0;
+  for (int it = 0; it < 24; it++) {
+    double m1 = lo + (hi - lo) / 3.0, m2 = hi - (hi - lo) / 3.0, n1[3], n2[3];
+    for (int t = 0; t < 3; t++) {
+      n1[t] = cos(m1) * u[t] + sin(m1) * w[t];
+      n2[t] = cos(m2) * u[t] + sin(m2) * w[t];
+    }
+    if (cyl_box_sep(cc, a, r, h, bc, A, bh, n1, &sg) < cyl_box_sep(cc, a, r, h, bc, A, bh, n2, &sg)) lo = m1;
+    else hi = m2;
+  }
+  double phi = 0.5 * (lo + hi);
+  for (int t = 0; t < 3; t++) n_out[t] = cos(phi) * u[t] + sin(phi) * w[t];
+}
+/* can an edge of the box parallel to axis k come within rb of point c? */
+static int edge_reach(const double c[3], const double bc[3], const double A[3][3], const double bh[3], int k, double rb) {
+  int i1 = (k + 1) % 3, i2 = (k + 2) % 3;
+  double d[3] = {c[0] - bc[0], c[1] - bc[1], c[2] - bc[2]};
+  double lk = dot3(d, A[k]), l1 = dot3(d, A[i1]), l2 = dot3(d, A[i2]);
+  double ek = fmax(0.0, fabs(lk) - bh[k]);
+  for (int e = 0; e < 4; e++) {
+    double o1 = (e & 1) ? bh[i1] : -bh[i1], o2 = (e & 2) ? bh[i2] : -bh[i2];
+    if (ek * ek + (l1 - o1) * (l1 - o1) + (l2 - o2) * (l2 - o2) <= rb * rb) return 1;
+  }
+  return 0;
+}
+static int cylinder_box(const or_data* d, const apm_model_t* m, int gc, int gb, or_contact* con) {
+  double bc[3], A[3][3], bh[3];
+  box_frame(d, m, gb, bc, A, bh);
+  const double* cc = d->geom_xpos[gc];
+  double a[3] = {d->geom_xmat[gc][2], d->geom_xmat[gc][5], d->geom_xmat[gc][8]};
+  double r = m->geom_size[gc][0], h = m->geom_size[gc][1];
+  double rbnd = sqrt(r * r + h * h);
+  double best = -1e300, nb[3] = {0, 0, 1};
+  for (int ax = 0; ax < 10; ax++) {
+    double n[3];
+    if (ax < 3) memcpy(n, A[ax], sizeof n);
+    else if (ax == 3) memcpy(n, a, sizeof n);
+    else if (ax < 7) {
+      cross3(n, a, A[ax - 4]);
+      double len = sqrt(dot3(n, n));
+      if (len < 1e-6) continue;
+      for (int t = 0; t < 3; t++) n[t] /= len;
+    } else {
+      if (!edge_reach(cc, bc, A, bh, ax - 7, rbnd)) continue;
+      edge_family(cc, a, r, h, bc, A, bh, ax - 7, n);
+    }
+    double cn = dot3(cc, n), ce = cyl_extent(a, r, h, n);
+    double cb = dot3(bc, n), rb = box_radius(A, bh, n);
+    if (sat_axis(n, cn - ce, cn + ce, cb - rb, cb + rb, &best, nb)) return 0;
+  }
+  /* witness: the cylinder's deepest point into the box (support along +nb), ties averaged */
+  double an = dot3(a, nb);
+  double sg = (2 * h * fabs(an) < OR_TIE) ? 0.0 : (an > 0 ? 1.0 : -1.0);
+  double rad[3] = {nb[0] - an * a[0], nb[1] - an * a[1], nb[2] - an * a[2]};
+  double rl = sqrt(dot3(rad, rad));
+  double rs = (r * rl < OR_TIE) ? 0.0 : r / rl;
+  con->dist = best;
+  for (int t = 0; t < 3; t++) con->pos[t] = cc[t] + sg * h * a[t] + rs * rad[t] + 0.5 * best * nb[t];
+  memcpy(con->frame, nb, sizeof nb);
+  return 1;
+}
+
 static void collision(const or_ctx* c, or_data* d) {
   const apm_model_t* m = c->m;
   d->ncon = 0;
@@ -716,6 +971,8 @@ static void collision(const or_ctx* c, or_data* d) {
       int n = 0;
       if (t1 == APM_GEOM_PLANE && t2 == APM_GEOM_CYLINDER) n = plane_cylinder(d, m, ga, gb, margin, tmp);
       else if (t1 == APM_GEOM_PLANE && t2 == APM_GEOM_MESH) n = plane_convex(c, d, ga, gb, margin, tmp);
+      else if (t1 == APM_GEOM_CYLINDER && t2 == APM_GEOM_BOX) n = cylinder_box(d, m, ga, gb, tmp);
+      else if (t1 == APM_GEOM_BOX && t2 == APM_GEOM_MESH) n = box_convex(c, d, ga, gb, tmp);
       else continue; /* pair types not present in this model class */
       for (int k = 0; k < n && d->ncon < OR_MAXCON; k++) {
         or_contact* cc = d->con + d->ncon++;
@@ -1116,6 +1373,26 @@ static double ray_cylinder(const double pos[3], const double mat[9], const doubl
     if (xx[i] >= 0 && fabs(lp[2] + xx[i] * lv[2]) <= size[1] && (x < 0 || xx[i] < x)) x = xx[i];
   return x;
 }
+/* ray vs box: nearest face-plane crossing x >= 0 whose point lies on the face (entry distance
+   from outside, exit distance from inside) */
+static double ray_box(const double pos[3], const double mat[9], const double size[3], const double pnt[3],
+                      const double vec[3]) {
+  if (ray_sphere_bound(pos, dot3(size, size), pnt, vec) < 0) return -1;
+  double lp[3], lv[3], x = -1;
+  ray_map(pos, mat, pnt, vec, lp, lv);
+  for (int i = 0; i < 3; i++) {
+    if (fabs(lv[i]) < mjMINVAL) continue;
+    for (int side = -1; side <= 1; side += 2) {
+      double sol = (side * size[i] - lp[i]) / lv[i];
+      if (sol < 0) continue;
+      int in = 1;
+      for (int j = 0; j < 3; j++)
+        if (j != i && fabs(lp[j] + sol * lv[j]) > size[j]) in = 0;
+      if (in && (x < 0 || sol < x)) x = sol;
+    }
+  }
+  return x;
+}
 /* ray vs triangle (a,b,c): Moller-Trumbore in the mesh frame; nearest x >= 0 or -1 */
 static double ray_triangle(const double a[3], const double b[3], const double cc[3], const double lp[3],
                            const double lv[3]) {
@@ -1177,6 +1454,7 @@ static double mj_ray(const or_ctx* c, const or_data* d, const double pnt[3], con
     switch (m->geom_type[g]) {
       case APM_GEOM_PLANE: nd = ray_plane(d->geom_xpos[g], d->geom_xmat[g], m->geom_size[g], pnt, vec); break;
       case APM_GEOM_CYLINDER: nd = ray_cylinder(d->geom_xpos[g], d->geom_xmat[g], m->geom_size[g], pnt, vec); break;
+      case APM_GEOM_BOX: nd = ray_box(d->geom_xpos[g], d->geom_xmat[g], m->geom_size[g], pnt, vec); break;
       case APM_GEOM_MESH: nd = ray_mesh(c, d, g, pnt, vec); break;
       default: nd = -1;
     }
@@ -1394,7 +1672,8 @@ static void env_reset(const or_ctx* c, or_data* d, double* st, int env, uint64_t
   double episode = st[ST_EPIS] + 1;
   memset(d, 0, sizeof(*d));
   memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
-  d->qpos[0] = 0; d->qpos[1] = 0; d->qpos[2] = 0.1; /* simple_map_spawner.py:43 (robot_pos=[0,0,0.1]) */
+  /* simple_map_spawner.py:43 (robot_pos=[0,0,0.1]); the obstacle scene's spawn is its own */
+  d->qpos[0] = m->spawn[0]; d->qpos[1] = m->spawn[1]; d->qpos[2] = m->spawn[2];
   d->qpos[3] = 1; d->qpos[4] = 0; d->qpos[5] = 0; d->qpos[6] = 0; /* :50 */
   /* mj_forward (simple_map_spawner.py:52): only its position stage feeds the env state / obs */
   kinematics(c, d);
@@ -1405,8 +1684,9 @@ static void env_reset(const or_ctx* c, or_data* d, double* st, int env, uint64_t
   philox4x32_10(ctr, key);
   double dd = 2.0 + 6.0 * u01(ctr[0]);
   double th = 2.0 * M_PI * u01(ctr[1]);
-  st[ST_GOAL] = dd * cos(th);
-  st[ST_GOAL + 1] = dd * sin(th);
+  /* goal = robot_start_position + offset (ackermann_env.py:167-172); start = chassis xpos */
+  st[ST_GOAL] = d->xpos[c->chassis_body][0] + dd * cos(th);
+  st[ST_GOAL + 1] = d->xpos[c->chassis_body][1] + dd * sin(th);
   memcpy(st + ST_REF, d->xpos[c->chassis_body], sizeof(double) * 3);
   st[ST_STEP] = 0;
   st[ST_EPIS] = episode;
@@ -1528,9 +1808,9 @@ int or_step_diag(const or_ctx* c, const double* st_in, const double* ctrl_in, ui
     o += 5;
   }
   memcpy(out + o, d->sensordata, sizeof(double) * m->nsensordata); o += m->nsensordata;
-  memcpy(out + o, d->xpos[1], sizeof(double) * 3); o += 3;
-  memcpy(out + o, d->xquat[1], sizeof(double) * 4); o += 4;
-  memcpy(out + o, d->subtree_com[1], sizeof(double) * 3); o += 3;
+  memcpy(out + o, d->xpos[c->chassis_body], sizeof(double) * 3); o += 3;
+  memcpy(out + o, d->xquat[c->chassis_body], sizeof(double) * 4); o += 4;
+  memcpy(out + o, d->subtree_com[c->chassis_body], sizeof(double) * 3); o += 3;
   /* efc rows */
   for (int r = 0; r < 96; r++) {
     if (r < d->nefc) {
@@ -1550,6 +1830,35 @@ int or_step_diag(const or_ctx* c, const double* st_in, const double* ctrl_in, ui
   memcpy(out + o, d->qvel, sizeof(double) * nv); o += nv;
   free(d);
   return o;
+}
+
+/* test export: the contacts mj_collision produces at qpos (mj_kinematics first); per contact
+   out[16] = geom1, geom2, dist, pos[3], frame[9], dim. Returns the number of contacts. */
+int or_contacts(const or_ctx* c, const double* qpos, double* out, int maxcon) {
+  or_data* d = (or_data*)calloc(1, sizeof(or_data));
+  memcpy(d->qpos, qpos, sizeof(double) * c->m->nq);
+  kinematics(c, d);
+  collision(c, d);
+  int n = d->ncon < maxcon ? d->ncon : maxcon;
+  for (int k = 0; k < n; k++) {
+    const or_contact* cc = d->con + k;
+    double* o = out + 16 * k;
+    o[0] = cc->geom1; o[1] = cc->geom2; o[2] = cc->dist;
+    memcpy(o + 3, cc->pos, sizeof(double) * 3);
+    memcpy(o + 6, cc->frame, sizeof(double) * 9);
+    o[15] = cc->dim;
+  }
+  free(d);
+  return n;
+}
+/* test export: mj_ray from pnt along unit vec (no body excluded) */
+double or_ray(const or_ctx* c, const double* qpos, const double pnt[3], const double vec[3]) {
+  or_data* d = (or_data*)calloc(1, sizeof(or_data));
+  memcpy(d->qpos, qpos, sizeof(double) * c->m->nq);
+  kinematics(c, d);
+  double r = mj_ray(c, d, pnt, vec, -1);
+  free(d);
+  return r;
 }
 
 /* ------------------------------------------------------------------ host twin of the C-ABI */

@@ -58,6 +58,11 @@ def lib():
         L.or_observe_raw.argtypes = [P, P, P, P, P, P, P, P, P, P]
         L.ackphys_step_cpu.argtypes = [P, i32] + [P] * 9 + [u32, u64, i32]
         L.ackphys_reset_cpu.argtypes = [P, i32, P, u64, P, P]
+        L.or_contacts.argtypes = [P, P, P, i32]
+        L.or_contacts.restype = i32
+        L.or_ray.argtypes = [P, P, P, P]
+        L.or_ray.restype = C.c_double
+        L.or_hull_features.argtypes = [P, i32, P, P, P, P]
         _lib = L
     return _lib
 
@@ -120,6 +125,23 @@ class Oracle:
         lib().or_observe_raw(self._ctx, _p(f(xpos)), _p(f(xquat)), _p(f(sensordata)), _p(f(goal)), _p(f(ref)),
                              _p(obs), _p(rew), C.byref(term), _p(info))
         return obs, float(rew[0]), bool(term.value), info
+
+    def contacts(self, qpos) -> np.ndarray:
+        """mj_collision at qpos: [ncon, 16] = geom1, geom2, dist, pos[3], frame[9], dim."""
+        q = np.ascontiguousarray(qpos, dtype=np.float64)
+        out = np.zeros((64, 16))
+        n = lib().or_contacts(self._ctx, _p(q), _p(out), 64)
+        return out[:n].copy()
+
+    def ray(self, qpos, pnt, vec) -> float:
+        f = lambda x: np.ascontiguousarray(x, dtype=np.float64)
+        return float(lib().or_ray(self._ctx, _p(f(qpos)), _p(f(pnt)), _p(f(vec))))
+
+    def hull_features(self, mesh: int):
+        fn, ed = np.zeros((96, 3)), np.zeros((96, 3))
+        nf, ne = C.c_int(0), C.c_int(0)
+        lib().or_hull_features(self._ctx, mesh, _p(fn), _p(ed), C.byref(nf), C.byref(ne))
+        return fn[: nf.value].copy(), ed[: ne.value].copy()
 
     def diag(self, state: np.ndarray, ctrl, flags: int = FLAG_CONTACTS, nv: int = 12, nq: int = 13,
              nsensordata: int = 77) -> dict:
