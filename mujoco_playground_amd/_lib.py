@@ -17,6 +17,9 @@ SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_q
            os.path.join(CSRC, "ackphys_model_gen.h"),
            os.path.join(REPO, "include", "ackphys.h"), os.path.join(REPO, "include", "ackphys_model.h")]
 BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
+# static-world scenes the kernels are specialised on: "flat" = ackermann_robot_v2.xml alone,
+# "obstacles" = the v2 robot in models/environments/ackermann_maze_flat.xml
+SCENES = {"flat": BLOB_PATH, "obstacles": os.path.join(PKG, "model", "assets", "ackermann_obstacles.apm")}
 PPO_LIB_PATH = os.path.join(CSRC, "build", "libackppo.so")
 PPO_SOURCES = [os.path.join(CSRC, "ackppo.hip"), os.path.join(REPO, "include", "ackppo.h")]
 
@@ -129,8 +132,10 @@ def ppo_check(rc: int, what: str):
         raise RuntimeError(f"{what} failed ({rc}): {ppo_lib().ackppo_last_error().decode()}")
 
 
-def load_blob() -> bytes:
-    with open(BLOB_PATH, "rb") as f:
+def load_blob(scene: str = "flat") -> bytes:
+    if scene not in SCENES:
+        raise ValueError(f"unknown scene {scene!r} (one of {sorted(SCENES)})")
+    with open(SCENES[scene], "rb") as f:
         return f.read()
 
 

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "ackphys_model_gen.h"
+#include "ackphys_scene_gen.h"
 
 // Diagnostic build only (-DAK_STAMPS): per-wave s_memtime phase stamps, never in the product.
 #ifdef AK_STAMPS
@@ -267,7 +268,35 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
   return ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
 }
 
+// ------------------------------------------------------------------ impedance / reference
+__device__ __forceinline__ float impedance_p(float pos, float d0, float dmax, float width, float mid, float pw) {
+  // getimpedance: solimp (d0, dmax, width, mid, power), margin 0
+  float x = fabsf(pos) / width;
+  if (x >= 1.0f) return dmax;
+  float y;
+  if (pw == 1.0f) y = x;
+  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1.0f);
+  else y = 1.0f - powf(1.0f - x, pw) / powf(1.0f - mid, pw - 1.0f);
+  float imp = d0 + y * (dmax - d0);
+  return fminf(fmaxf(imp, 0.0001f), 0.9999f);
+}
+// joint / dof / equality rows
+__device__ __forceinline__ float impedance(float pos) {
+  return impedance_p(pos, SOLIMP[0], SOLIMP[1], SOLIMP[2], SOLIMP[3], SOLIMP[4]);
+}
+// K, B from solref (refsafe: timeconst >= 2*dt)
+__device__ __forceinline__ void ref_kb_p(float sr0, float sr1, float dmax, float& K, float& B) {
+  const float tc = sr0 > 2.0f * DT ? sr0 : 2.0f * DT;
+  const float dr = sr1;
+  K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
+  B = 2.0f / (dmax * tc);
+}
+__device__ __forceinline__ void ref_kb(float& K, float& B) { ref_kb_p(SOLREF[0], SOLREF[1], SOLIMP[1], K, B); }
+
+#include "ackphys_scene.inc"
+
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
+template <int SC>
 __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
                           const float ref[3], const Soa& dst, uint32_t vo, const EnvParams& prm) {
   float head[7];
@@ -278,7 +307,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   float minl = 3.0e38f, v71 = -1.0f;
 #pragma unroll
   for (int i = 10; i < 72; i++) {
-    float v = ray_floor(p, R, i);
+    float v = ray_scene<SC>(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
     stf(dst, i, vo, v);
     minl = fminf(minl, v);
     v71 = v;
@@ -297,28 +326,6 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   r -= 0.01f;
   o.reward = r;
   return o;
-}
-
-// ------------------------------------------------------------------ impedance / reference
-__device__ __forceinline__ float impedance(float pos) {
-  // getimpedance: solimp (d0, dmax, width, mid, power), margin 0
-  const float d0 = SOLIMP[0], dmax = SOLIMP[1], width = SOLIMP[2], mid = SOLIMP[3], pw = SOLIMP[4];
-  float x = fabsf(pos) / width;
-  if (x >= 1.0f) return dmax;
-  float y;
-  if (pw == 1.0f) y = x;
-  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1.0f);
-  else y = 1.0f - powf(1.0f - x, pw) / powf(1.0f - mid, pw - 1.0f);
-  float imp = d0 + y * (dmax - d0);
-  return fminf(fmaxf(imp, 0.0001f), 0.9999f);
-}
-// K, B from solref (refsafe: timeconst >= 2*dt)
-__device__ __forceinline__ void ref_kb(float& K, float& B) {
-  const float dmax = SOLIMP[1];
-  const float tc = SOLREF[0] > 2.0f * DT ? SOLREF[0] : 2.0f * DT;
-  const float dr = SOLREF[1];
-  K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
-  B = 2.0f / (dmax * tc);
 }
 
 // ------------------------------------------------------------------ 12x12 Cholesky
@@ -1321,16 +1328,20 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 }
 
 // ------------------------------------------------------------------ state I/O helpers
+template <int SC>
 __device__ __forceinline__ void reset_pose(float qpos[13], float qvel[NV], float warm[NV]) {
   // SimpleMapSpawner.load_random_environment: qpos0 with chassis at (0,0,0.1), identity quat
+  // (the obstacle scene spawns at its own free cell, Scene<1>)
 #pragma unroll
   for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
-  qpos[0] = 0.0f; qpos[1] = 0.0f; qpos[2] = 0.1f;
+  qpos[0] = Scene<SC>::SPX; qpos[1] = Scene<SC>::SPY; qpos[2] = Scene<SC>::SPZ;
   qpos[3] = 1.0f; qpos[4] = 0.0f; qpos[5] = 0.0f; qpos[6] = 0.0f;
 #pragma unroll
   for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
 }
 
+// goal = robot_start_position + (d cos th, d sin th) (ackermann_env.py:167-172)
+template <int SC>
 __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_t episode, float& gx, float& gy) {
   uint32_t c[4] = {(uint32_t)genv, episode, 0u, 0u};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -1338,15 +1349,20 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
   float th = 6.283185307179586f * u01(c[1]);
   gx = d * cosf(th);
   gy = d * sinf(th);
+  if constexpr (SC != 0) {
+    gx += Scene<SC>::SPX;
+    gy += Scene<SC>::SPY;
+  }
 }
 
 // reset env e: writes state words + observation
+template <int SC>
 __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint32_t vo, uint64_t seed, int64_t genv,
                                           uint32_t episode, const EnvParams& prm) {
   float qpos[13], qvel[NV], warm[NV];
-  reset_pose(qpos, qvel, warm);
+  reset_pose<SC>(qpos, qvel, warm);
   float gx, gy;
-  goal_sample(seed, genv, episode, gx, gy);
+  goal_sample<SC>(seed, genv, episode, gx, gy);
   float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
   normq(q);
   float R[9];
@@ -1365,7 +1381,7 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
   for (int k = 0; k < 3; k++) stf(state, ST_REF + k, vo, ref[k]);
   stf(state, ST_STEP, vo, __uint_as_float(0u));
   stf(state, ST_EPIS, vo, __uint_as_float(episode));
-  observe(qpos, q, R, gx, gy, ref, obs, vo, prm);
+  observe<SC>(qpos, q, R, gx, gy, ref, obs, vo, prm);
 }
 
 }  // namespace ak
@@ -1449,7 +1465,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     const bool done_pre = oh.term || trunc;
     const bool autoreset = (A.flags & F_AUTORESET) && done_pre;
     const Soa obs = soa(A.obs, NOBS, n);
-    ObsOut o = observe(p, q, R, gx, gy, ref, obs, vo, A.prm);
+    ObsOut o = observe<0>(p, q, R, gx, gy, ref, obs, vo, A.prm);
     if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset);
     stf(soa(A.reward, 1, n), 0, vo, o.reward);
     stb(soa(A.term, 1, n, 1), (uint32_t)e, o.term ? 1 : 0);
@@ -1477,7 +1493,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
 
     STAMP(9);
     if (autoreset) {
-      reset_env(st, obs, vo, A.seed, A.env_offset + e, episode + 1, A.prm);
+      reset_env<0>(st, obs, vo, A.seed, A.env_offset + e, episode + 1, A.prm);
       return;
     }
 #pragma unroll
@@ -1492,16 +1508,26 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) ackphys_reset_kernel(const uint8_t* mask, float* state, float* obs,
-                                                                       int n, uint64_t seed, int64_t env_offset,
-                                                                       EnvParams prm) {
+template <int SC>
+__device__ __forceinline__ void reset_body(const uint8_t* mask, float* state, float* obs, int n, uint64_t seed,
+                                           int64_t env_offset, const EnvParams& prm) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   if (mask && !mask[e]) return;
   const Soa st = soa(state, NSTATE, n), ob = soa(obs, NOBS, n);
   const uint32_t vo = 4u * (uint32_t)e;
   const uint32_t episode = __float_as_uint(ldf(st, ST_EPIS, vo)) + 1u;
-  reset_env(st, ob, vo, seed, env_offset + e, episode, prm);
+  reset_env<SC>(st, ob, vo, seed, env_offset + e, episode, prm);
+}
+extern "C" __global__ void __launch_bounds__(256) ackphys_reset_kernel(const uint8_t* mask, float* state, float* obs,
+                                                                       int n, uint64_t seed, int64_t env_offset,
+                                                                       EnvParams prm) {
+  reset_body<0>(mask, state, obs, n, seed, env_offset, prm);
+}
+extern "C" __global__ void __launch_bounds__(256) ackphys_reset_obst_kernel(const uint8_t* mask, float* state,
+                                                                            float* obs, int n, uint64_t seed,
+                                                                            int64_t env_offset, EnvParams prm) {
+  reset_body<1>(mask, state, obs, n, seed, env_offset, prm);
 }
 
 extern "C" __global__ void __launch_bounds__(256) ackphys_actions_kernel(float* actions, int n, int k_steps,
@@ -1528,6 +1554,7 @@ struct ackphys_ctx {
   int64_t env_offset;
   ak::EnvParams prm;
   int variant;  // ACKPHYS_VARIANT_LANE (1 lane/env) or ACKPHYS_VARIANT_QUAD (4 lanes/env)
+  int scene;    // 0: ackermann_robot_v2 (floor only); 1: obstacle scene (floor + boxes)
 };
 
 static thread_local char g_err[512];
@@ -1556,7 +1583,9 @@ int ackphys_diag_set_stamps(void* buf) {
 }
 #endif
 
-const char* ackphys_version(void) { return "ackphys 0.2 (gfx950; step kernels: lane-per-env, quad-per-env)"; }
+const char* ackphys_version(void) {
+  return "ackphys 0.3 (gfx950; step kernels: lane-per-env, quad-per-env; scenes: v2 floor, obstacles)";
+}
 uint64_t ackphys_model_fnv(void) { return apg::MODEL_FNV; }
 
 int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device, ackphys_t** out) {
@@ -1566,8 +1595,12 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
   const apm_model_t* m = (const apm_model_t*)model_blob;
   if (m->magic != APM_MAGIC || m->version != APM_VERSION || m->nbytes != nbytes)
     return fail(ACKPHYS_EMODEL, "model blob: bad magic/version/size");
-  if (fnv1a64((const unsigned char*)model_blob, nbytes) != apg::MODEL_FNV)
-    return fail(ACKPHYS_EMODEL, "model blob does not match the model these kernels were specialised on "
+  const uint64_t h = fnv1a64((const unsigned char*)model_blob, nbytes);
+  int scene = -1;
+  if (h == apg::MODEL_FNV) scene = 0;
+  else if (h == apg::scene1::SCENE_FNV) scene = 1;
+  if (scene < 0)
+    return fail(ACKPHYS_EMODEL, "model blob does not match a model these kernels were specialised on "
                                 "(regenerate with python -m mujoco_playground_amd.model.build and rebuild)");
   if (n_env <= 0) return fail(ACKPHYS_EINVAL, "n_env must be positive");
   // buffer descriptors address [79][N] float arrays with 31-bit byte ranges
@@ -1582,6 +1615,7 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
   c->env_offset = 0;
   c->prm = ak::EnvParams{1000, 0.5f, 0.15f, 1.0f, 1.0f};  // AckermannRobotEnv defaults
   c->variant = ACKPHYS_VARIANT_AUTO;
+  c->scene = scene;
   *out = c;
   return ACKPHYS_OK;
 }
@@ -1627,7 +1661,12 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
   // contacts the replicated serial core dominates and one lane per env is marginally faster.
   const bool quad = ctx->variant == ACKPHYS_VARIANT_QUAD ||
                     (ctx->variant == ACKPHYS_VARIANT_AUTO && (flags & ACKPHYS_CONTACTS));
-  if (quad) {
+  if (ctx->scene == 1) {  // the obstacle scene is specialised on the quad mapping only
+    if (ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
+      return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
+    int blocks = (ctx->n_env + 15) / 16;
+    hipLaunchKernelGGL(ackphys_step_obst_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  } else if (quad) {
     int blocks = (ctx->n_env + 15) / 16;
     hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
   } else {
@@ -1645,8 +1684,12 @@ int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* sta
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hipfail(e, "hipSetDevice");
   int blocks = (ctx->n_env + 255) / 256;
-  hipLaunchKernelGGL(ackphys_reset_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
-                     ctx->n_env, seed, ctx->env_offset, ctx->prm);
+  if (ctx->scene == 1)
+    hipLaunchKernelGGL(ackphys_reset_obst_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
+                       ctx->n_env, seed, ctx->env_offset, ctx->prm);
+  else
+    hipLaunchKernelGGL(ackphys_reset_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
+                       ctx->n_env, seed, ctx->env_offset, ctx->prm);
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_reset_kernel launch");
   return ACKPHYS_OK;

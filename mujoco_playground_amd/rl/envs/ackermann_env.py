@@ -19,7 +19,7 @@ class AckermannRobotEnv:
 
     def __init__(self, map_spawner=None, max_episode_steps=1000, goal_distance_threshold=0.5,
                  collision_threshold=0.15, max_linear_velocity=1.0, max_angular_velocity=1.0, render_mode=None,
-                 device="cuda:0", contacts: bool = True):
+                 device="cuda:0", contacts: bool = True, scene: str = "flat"):
         # render_mode="human": the reference opens a passive MuJoCo viewer (out of scope here: no
         # window) and runs mj_forward after every mj_step (ackermann_env.py:202-207), so its
         # observations/rewards come from the post-step pose. That numerical effect is kept.
@@ -36,7 +36,7 @@ class AckermannRobotEnv:
                                         collision_threshold=collision_threshold,
                                         max_linear_velocity=max_linear_velocity,
                                         max_angular_velocity=max_angular_velocity,
-                                        poststep_obs=(render_mode == "human"))
+                                        poststep_obs=(render_mode == "human"), scene=scene)
         self._rng = np.random.default_rng()
         self.step_count = 0
         self.goal_position = None
@@ -50,9 +50,10 @@ class AckermannRobotEnv:
         self.step_count = 0
         st = self._sim.state[:, 0].cpu().numpy()
         self.goal_position = st[37:39].astype(np.float64)
-        self.robot_start_position = np.zeros(2)
+        self.robot_start_position = st[39:41].astype(np.float64)   # odometry reference = spawn (x, y)
         obs = self._sim.obs_soa[:, 0].cpu().numpy().astype(np.float32)
-        info = {"map_name": "simple_floor", "goal_position": self.goal_position.tolist(),
+        info = {"map_name": "simple_floor" if self._sim.scene == "flat" else "ackermann_maze_flat",
+                "goal_position": self.goal_position.tolist(),
                 "start_position": self.robot_start_position.tolist()}
         return obs, info
 

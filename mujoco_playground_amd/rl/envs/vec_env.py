@@ -18,7 +18,8 @@ class AckermannVecEnv:
     def __init__(self, num_envs: int = 4096, device="cuda:0", seed: int = 0, contacts: bool = True,
                  env_offset: int = 0, max_episode_steps: int = 1000, goal_distance_threshold: float = 0.5,
                  collision_threshold: float = 0.15, max_linear_velocity: float = 1.0,
-                 max_angular_velocity: float = 1.0, render_mode=None, variant: str = "auto"):
+                 max_angular_velocity: float = 1.0, render_mode=None, variant: str = "auto",
+                 scene: str = "flat"):
         self.num_envs = int(num_envs)
         self.observation_space = spaces.observation_space()
         self.action_space = spaces.action_space()
@@ -28,7 +29,7 @@ class AckermannVecEnv:
                                        collision_threshold=collision_threshold,
                                        max_linear_velocity=max_linear_velocity,
                                        max_angular_velocity=max_angular_velocity, variant=variant,
-                                       poststep_obs=(render_mode == "human"))
+                                       poststep_obs=(render_mode == "human"), scene=scene)
         self.device = self.sim.device
         self._actions = None
         self._ep_ret = torch.zeros(self.num_envs, device=self.device)

@@ -28,7 +28,7 @@ class BatchedAckermannSim:
                  env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
                  goal_distance_threshold: float = 0.5, collision_threshold: float = 0.15,
                  max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0, variant: str = "auto",
-                 poststep_obs: bool = False):
+                 poststep_obs: bool = False, scene: str = "flat"):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
@@ -38,7 +38,8 @@ class BatchedAckermannSim:
         # render_mode="human" semantics: obs/reward from the post-step pose (ackermann_env.py:202-207)
         self.poststep_obs = bool(poststep_obs)
         L = _lib.lib()
-        blob = model_blob if model_blob is not None else _lib.load_blob()
+        self.scene = scene
+        blob = model_blob if model_blob is not None else _lib.load_blob(scene)
         ctx = C.c_void_p()
         _lib.check(L.ackphys_create(blob, len(blob), self.n, self.device.index or 0, C.byref(ctx)), "ackphys_create")
         self._ctx = ctx
