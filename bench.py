@@ -10,7 +10,9 @@ action batches are drawn on device from Philox (seed 0; counter = (env, step)).
 Prints ONE JSON line (rank 0).
 
 Workload (value): BASELINE.json configs[1] -- 4096 envs/GPU, random ctrl, contacts disabled.
-The contacts-enabled variant (configs[2]) is reported under "secondary".
+The contacts-enabled variant (configs[2]) is reported under "secondary"; the obstacle scene
+(configs[4]'s world: the v2 robot in models/environments/ackermann_maze_flat.xml, 38 boxes)
+under "obstacles" (env steps, contacts on) and its PPO rollout under "obstacles.ppo".
 """
 from __future__ import annotations
 
@@ -41,9 +43,9 @@ def algorithmic_bytes_per_env_step() -> int:
     return 176 + 8 + 16 + 152 + 316 + 4 + 2 + 16
 
 
-def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto"):
+def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat"):
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
-                              env_offset=shard.env_offset(rank, n_env), variant=variant)
+                              env_offset=shard.env_offset(rank, n_env), variant=variant, scene=scene)
     sim.reset()
     actions = sim.random_actions(warmup + steps, seed=seed)
     for k in range(warmup):
@@ -68,13 +70,14 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     return sim, elapsed, kern_ms, shard.summarize_returns(gathered), actions
 
 
-def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_epochs=10, seed=0):
+def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_epochs=10, seed=0, scene="flat"):
     """BASELINE configs[3]: PPO rollout on the env shard (contacts enabled, SB3 PPO('MlpPolicy')
     semantics on libackppo.so). One warm-up iteration, then `iters` timed iterations of
     collect_rollouts (n_steps policy+env steps) + train (n_epochs over minibatches)."""
     from mujoco_playground_amd.rl import AckermannVecEnv
     from mujoco_playground_amd.rl.ppo import PPO
-    venv = AckermannVecEnv(n_env, device=device, seed=seed, contacts=True, env_offset=shard.env_offset(rank, n_env))
+    venv = AckermannVecEnv(n_env, device=device, seed=seed, contacts=True, env_offset=shard.env_offset(rank, n_env),
+                           scene=scene)
     model = PPO("MlpPolicy", venv, n_steps=n_steps, batch_size=batch_size, n_epochs=n_epochs, seed=seed,
                 ent_coef=0.0, world=world, rank=rank)
     model.collect_rollouts()
@@ -102,8 +105,8 @@ def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_
             "rollout_env_steps_per_s": n_steps * n_env * world / (roll_ms * 1e-3),
             "rollout_ms": roll_ms, "update_ms": train_ms, "minibatch_updates_per_iter": nmb * n_epochs,
             "update_us_per_minibatch": train_ms * 1e3 / (nmb * n_epochs),
-            "config": f"{n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} ranks, "
-                      f"{n_epochs} epochs, contacts on, {iters} timed iterations after 1 warm-up",
+            "config": f"{scene} scene, {n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} "
+                      f"ranks, {n_epochs} epochs, contacts on, {iters} timed iterations after 1 warm-up",
             "last_logger": {k: v for k, v in model.logger.items() if isinstance(v, (int, float)) or v is None}}
 
 
@@ -222,6 +225,7 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane", "lane16"], help="step-kernel lane mapping")
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO-rollout leg (BASELINE configs[3])")
+    ap.add_argument("--no-obstacles", action="store_true", help="skip the obstacle-scene leg (configs[4] world)")
     a = ap.parse_args()
     rank, world, local = shard.init()
     device = shard.device_for(local)
@@ -237,6 +241,14 @@ def main():
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
                      "kernel_ms": km2}
     ppo = None if a.no_ppo else run_ppo(a.envs, rank, world, device)
+    obstacles = None
+    if not a.no_obstacles:
+        _, el3, km3, rets3, _ = run_gpu(a.envs, a.steps, a.warmup, True, rank, world, device, scene="obstacles")
+        obstacles = {"workload": f"v2 robot in ackermann_maze_flat.xml (38 static boxes), {a.envs} envs/GPU, "
+                                 "random ctrl, contacts enabled, spawn at the scene's free cell",
+                     "value": total_envs * a.steps / el3, "unit": "env-steps/s", "ms_per_step": el3 * 1e3 / a.steps,
+                     "kernel": "ackphys_step_obst_kernel", "kernel_ms": km3, "episodes": rets3,
+                     "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
     parity = base = None
     if rank == 0 and not a.no_cpu:
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
@@ -269,6 +281,7 @@ def main():
                          "algorithmic_bytes_per_env_step": bpe,
                          "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
+            "obstacles": obstacles,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

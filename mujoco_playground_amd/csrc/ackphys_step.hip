@@ -1340,8 +1340,8 @@ __device__ __forceinline__ void reset_pose(float qpos[13], float qvel[NV], float
   for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
 }
 
-// goal = robot_start_position + (d cos th, d sin th) (ackermann_env.py:167-172)
-template <int SC>
+// goal = robot_start_position + (d cos th, d sin th) (ackermann_env.py:167-172) in the odometry
+// frame, where the start position is (0, 0) whatever the spawn point (odometry.py:62-103)
 __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_t episode, float& gx, float& gy) {
   uint32_t c[4] = {(uint32_t)genv, episode, 0u, 0u};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -1349,10 +1349,6 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
   float th = 6.283185307179586f * u01(c[1]);
   gx = d * cosf(th);
   gy = d * sinf(th);
-  if constexpr (SC != 0) {
-    gx += Scene<SC>::SPX;
-    gy += Scene<SC>::SPY;
-  }
 }
 
 // reset env e: writes state words + observation
@@ -1362,7 +1358,7 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
   float qpos[13], qvel[NV], warm[NV];
   reset_pose<SC>(qpos, qvel, warm);
   float gx, gy;
-  goal_sample<SC>(seed, genv, episode, gx, gy);
+  goal_sample(seed, genv, episode, gx, gy);
   float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
   normq(q);
   float R[9];

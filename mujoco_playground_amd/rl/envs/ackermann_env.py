@@ -50,7 +50,7 @@ class AckermannRobotEnv:
         self.step_count = 0
         st = self._sim.state[:, 0].cpu().numpy()
         self.goal_position = st[37:39].astype(np.float64)
-        self.robot_start_position = st[39:41].astype(np.float64)   # odometry reference = spawn (x, y)
+        self.robot_start_position = np.zeros(2)   # odometry position at reset (odometry.py measures from it)
         obs = self._sim.obs_soa[:, 0].cpu().numpy().astype(np.float32)
         info = {"map_name": "simple_floor" if self._sim.scene == "flat" else "ackermann_maze_flat",
                 "goal_position": self.goal_position.tolist(),

@@ -1684,9 +1684,11 @@ static void env_reset(const or_ctx* c, or_data* d, double* st, int env, uint64_t
   philox4x32_10(ctr, key);
   double dd = 2.0 + 6.0 * u01(ctr[0]);
   double th = 2.0 * M_PI * u01(ctr[1]);
-  /* goal = robot_start_position + offset (ackermann_env.py:167-172); start = chassis xpos */
-  st[ST_GOAL] = d->xpos[c->chassis_body][0] + dd * cos(th);
-  st[ST_GOAL + 1] = d->xpos[c->chassis_body][1] + dd * sin(th);
+  /* goal = robot_start_position + offset (ackermann_env.py:167-172), in the odometry frame:
+     robot_start_position is the odometry position at reset, i.e. (0, 0) (odometry.py:62-103
+     measures from the reset pose), whatever the spawn point */
+  st[ST_GOAL] = dd * cos(th);
+  st[ST_GOAL + 1] = dd * sin(th);
   memcpy(st + ST_REF, d->xpos[c->chassis_body], sizeof(double) * 3);
   st[ST_STEP] = 0;
   st[ST_EPIS] = episode;

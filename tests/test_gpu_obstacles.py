@@ -93,7 +93,7 @@ def wall_states(n, lo, hi, rng, gap=(0.19, 0.26), speed=0.25, clearance=0.185):
         st[e, 0:3] = [x, y, 0.0649]
         st[e, 3:7] = _yaw_quat(yaw)
         st[e, 13:15] = -speed * np.array([nx, ny])
-        st[e, 37:39] = [x + 3.0, y + 1.0]
+        st[e, 37:39] = [3.0, 1.0]   # odometry frame (relative to the episode start)
         st[e, 39:42] = [x, y, 0.0649]
         st[e, 43] = 1
     return st
