@@ -26,9 +26,8 @@ DIAG_LEN = 8192
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB_PATH) or (
-            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "ackphys_oracle.c"))):
-        subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+    """make (incremental: rebuilds when ackphys_oracle.c or a header it includes changed)."""
+    subprocess.run(["make", "-C", HERE] + (["-B"] if force else []), check=True, capture_output=True)
     return LIB_PATH
 
 
