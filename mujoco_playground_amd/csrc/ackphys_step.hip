@@ -159,6 +159,19 @@ __device__ __forceinline__ void cross(float r[3], const float a[3], const float 
 __device__ __forceinline__ float dot(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }  // NaN or huge
 
+// Reciprocal / division / square-root helpers. Measured on MI355X (tools/variant_sweep.sh): the
+// hardware v_rcp/v_rsq/v_sqrt forms and a Cody-Waite/Cephes sincos cut instructions but made the
+// lane kernel's register allocation worse (36.7 -> 37.9 us/step contacts off), so the IEEE forms stay.
+__device__ __forceinline__ float frcp(float x) { return 1.0f / x; }
+__device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
+__device__ __forceinline__ float frsq(float x) { return 1.0f / sqrtf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ void fsincos(float x, float& s, float& c) { sincosf(x, &s, &c); }
+// wrap to [-pi, pi] (atan2(sin a, cos a) of the reference) for |a| <= 3 pi
+__device__ __forceinline__ float wrap_pi(float a) {
+  return fmaf(__builtin_rintf(a * 0.159154943091895336f), -6.28318530717958648f, a);
+}
+
 // Philox4x32-10 (Random123); identical to oracle/ackphys_oracle.c
 __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -177,34 +190,34 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // float64 exactly like the reference (its thresholds 1e-6 / 1e-5 sit on f64 values).
 __device__ __forceinline__ void controller(float a0f, float a1f, float max_lin, float max_ang, float ctrl[3], bool& bad) {
   // np.clip on the float32 action, then action * max_velocity: float32 x Python float stays
-  // float32 under NumPy 2 promotion (ackermann_env.py:190-194); controller works in float64
+  // float32 under NumPy 2 promotion (ackermann_env.py:190-194); controller works in float64.
+  // Restated without the f64 atan/tan round trip: with y = L om / den, delta = clip(atan(y), +-35 deg)
+  // and tan(delta) = y inside the clip (tan(35 deg) outside), |delta| < 1e-6 <=> |y| < 1e-6 (to 3e-19),
+  // R = L / tan(delta) is finite (|R| > 0.28 > eps) unless |tan(delta)| <= eps -- the reference's
+  // 0 * inf = NaN path, which zeroes ctrl -- so v (R -+ T/2) / R = v (1 -+ tan(delta) T / 2L).
   a0f = a0f < -1.0f ? -1.0f : (a0f > 1.0f ? 1.0f : a0f);
   a1f = a1f < -1.0f ? -1.0f : (a1f > 1.0f ? 1.0f : a1f);
   const double L = 0.20, T = 0.174, rw = 0.0325, eps = 1e-5;
-  double v = (double)(a0f * max_lin), om = (double)(a1f * max_ang), delta;
-  if (fabs(om) < 1e-6) delta = 0.0;
-  else {
-    double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
-    delta = atan((L * om) / den);
+  const double TAN_LIM = 0.70020753820970977;  // tan(35 deg) (controller.py:112)
+  const double v = (double)(a0f * max_lin), om = (double)(a1f * max_ang);
+  double y = 0.0;
+  if (!(fabs(om) < 1e-6)) {
+    const double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
+    y = (L * om) / den;
   }
-  const double lim = 35.0 * (3.141592653589793 / 180.0);
-  delta = delta < -lim ? -lim : (delta > lim ? lim : delta);
-  double vl, vr;
-  if (fabs(delta) < 1e-6) vl = vr = v;
-  else {
-    double t = tan(delta);
-    double R = fabs(t) > eps ? L / t : __builtin_inf();
-    double wt = fabs(R) > eps ? v / R : 0.0;
-    vl = wt * (R - T / 2.0);   // 0*inf = NaN, as in the reference
-    vr = wt * (R + T / 2.0);
+  double vl = v, vr = v;
+  if (!(fabs(y) < 1e-6)) {
+    const double t = fabs(y) > TAN_LIM ? copysign(TAN_LIM, y) : y;
+    const double k = fabs(t) > eps ? t * (T / (2.0 * L)) : __builtin_nan("");
+    vl = v * (1.0 - k);
+    vr = v * (1.0 + k);
   }
-  double wl = vl / rw, wr = vr / rw;
-  double c0 = delta < -0.61 ? -0.61 : (delta > 0.61 ? 0.61 : delta);
+  const double wl = vl * (1.0 / rw), wr = vr * (1.0 / rw);
+  const float c0 = fminf(fmaxf(atanf((float)y), -0.61f), 0.61f);  // clip(delta, +-0.61)
   double c1 = (wl != wl) ? wl : (wl < -50 ? -50 : (wl > 50 ? 50 : wl));
   double c2 = (wr != wr) ? wr : (wr < -50 ? -50 : (wr > 50 ? 50 : wr));
-  bad = !(fabs(c0) <= 1e10) || !(fabs(c1) <= 1e10) || !(fabs(c2) <= 1e10);
-  if (bad) c0 = c1 = c2 = 0.0;  // MuJoCo zeroes ctrl on bad values
-  ctrl[0] = (float)c0; ctrl[1] = (float)c1; ctrl[2] = (float)c2;
+  bad = (c0 != c0) || !(fabs(c1) <= 1e10) || !(fabs(c2) <= 1e10);
+  ctrl[0] = bad ? 0.0f : c0; ctrl[1] = bad ? 0.0f : (float)c1; ctrl[2] = bad ? 0.0f : (float)c2;  // MuJoCo zeroes bad ctrl
 }
 
 // ------------------------------------------------------------------ kinematics
@@ -215,9 +228,9 @@ __device__ __forceinline__ void quat_R(const float q[4], float R[9]) {
   R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
 }
 __device__ __forceinline__ void normq(float q[4]) {
-  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  float n = fsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
-  else { float inv = 1.0f / n; q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv; }
+  else { float inv = frcp(n); q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv; }
 }
 // rotate v about unit axis s by angle (Rodrigues): the steer rotation of front-wheel frames
 __device__ __forceinline__ void rot_axis(float r[3], const float s[3], const float v[3], float c, float sn) {
@@ -243,7 +256,7 @@ __device__ __forceinline__ ObsOut observe_head(const float p[3], const float q[4
   float dx = gx - x, dy = gy - y;
   float dist = sqrtf(dx * dx + dy * dy);
   float ang = atan2f(dy, dx) - yaw;
-  ang = atan2f(sinf(ang), cosf(ang));
+  ang = wrap_pi(ang);
   out8[0] = x; out8[1] = y; out8[2] = yaw; out8[3] = dx; out8[4] = dy; out8[5] = dist; out8[6] = ang;
   ObsOut o;
   o.dist = dist;
@@ -271,7 +284,7 @@ __device__ __forceinline__ float ray_floor(const float p[3], const float R[9], i
 // ------------------------------------------------------------------ impedance / reference
 __device__ __forceinline__ float impedance_p(float pos, float d0, float dmax, float width, float mid, float pw) {
   // getimpedance: solimp (d0, dmax, width, mid, power), margin 0
-  float x = fabsf(pos) / width;
+  float x = fabsf(pos) * (1.0f / width);
   if (x >= 1.0f) return dmax;
   float y;
   if (pw == 1.0f) y = x;
@@ -288,8 +301,8 @@ __device__ __forceinline__ float impedance(float pos) {
 __device__ __forceinline__ void ref_kb_p(float sr0, float sr1, float dmax, float& K, float& B) {
   const float tc = sr0 > 2.0f * DT ? sr0 : 2.0f * DT;
   const float dr = sr1;
-  K = 1.0f / (dmax * dmax * tc * tc * dr * dr);
-  B = 2.0f / (dmax * tc);
+  K = frcp(dmax * dmax * tc * tc * dr * dr);
+  B = fdiv(2.0f, dmax * tc);
 }
 __device__ __forceinline__ void ref_kb(float& K, float& B) { ref_kb_p(SOLREF[0], SOLREF[1], SOLIMP[1], K, B); }
 
@@ -328,50 +341,153 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   return o;
 }
 
-// ------------------------------------------------------------------ 12x12 Cholesky
-// L L^T in the lower triangle; the diagonal holds 1/L_jj (solves multiply, never divide)
-__device__ __forceinline__ bool chol12(float A[NV][NV]) {
-  bool ok = true;
+// ------------------------------------------------------------------ structured factorisation
+// The Hessians of this model are sparse with a fixed structure: a hinge couples only to the free
+// joint's dofs (wheel / steer inertia about the chassis; contact rows of its own wheel) and to the
+// other hinge of its wheel (steer <-> spin) or the steer equality (steer L <-> steer R). With the
+// hinges eliminated first (rear spins, front spins, front steers), then the free joint's linear and
+// angular dofs, the Cholesky factor has no fill outside the 6x6 free-joint block. The patterns
+// below are derived at compile time; skipped terms are structural zeros (0 * finite), so results
+// equal the dense factorisation up to the reordering's rounding.
+struct SymPat { bool nz[NV][NV]; };
+// per-mapping choice between the structured (KIND) and the dense (3) factorisation; picked by
+// measurement (tools/variant_sweep.sh): the lane kernel is faster structured, the quad kernels dense
+#ifndef AK_LANE_DENSE
+#define AK_LANE_DENSE 0
+#endif
+#ifndef AK_QUAD_DENSE
+#define AK_QUAD_DENSE 1  // measured: dense 90.2 us vs structured 95.5 us per contacts-on step
+#endif
+#define LANE_K(k) (AK_LANE_DENSE ? 3 : (k))
+#define QUAD_K(k) (AK_QUAD_DENSE ? 3 : (k))
+#ifdef AK_ORD_IDENT
+constexpr int ORD[NV] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+#else
+constexpr int ORD[NV] = {W_SPIN_DOF[0], W_SPIN_DOF[1], W_SPIN_DOF[2], W_SPIN_DOF[3], W_STEER_DOF[2],
+                         W_STEER_DOF[3], 0, 1, 2, 3, 4, 5};
+#endif
+static_assert(W_STEER_DOF[0] < 0 && W_STEER_DOF[1] < 0 && W_STEER_DOF[2] >= 6 && W_STEER_DOF[3] >= 6,
+              "factorisation order assumes rear wheels without steering and two steered front wheels");
+constexpr bool ord_is_perm() {
+  bool seen[NV] = {};
+  for (int i = 0; i < NV; i++) {
+    if (ORD[i] < 0 || ORD[i] >= NV || seen[ORD[i]]) return false;
+    seen[ORD[i]] = true;
+  }
+  return true;
+}
+static_assert(ord_is_perm(), "ORD must be a permutation of the dofs");
+// kind 0: mass matrix (a0, implicit Euler); 1: + scalar rows (equality, friction loss, limits);
+// 2: + contact rows (every wheel / plate contact couples the free joint and its wheel's hinges)
+constexpr SymPat make_pat(int kind) {
+  SymPat p{};
+  auto set = [&p](int a, int b) { p.nz[a][b] = true; p.nz[b][a] = true; };
+  for (int i = 0; i < NV; i++) set(i, i);
+  if (kind == 3) {  // dense (the factorisation still runs in ORD order)
+    for (int i = 0; i < NV; i++)
+      for (int j = 0; j < NV; j++) set(i, j);
+  }
+  for (int a = 3; a < 6; a++)
+    for (int b = 0; b < 6; b++) set(a, b);  // I_O and m [c]x
+  for (int w = 0; w < 4; w++) {
+    for (int a = 3; a < 6; a++) {
+      set(W_SPIN_DOF[w], a);
+      if (W_STEER_DOF[w] >= 0) set(W_STEER_DOF[w], a);
+    }
+    if (W_STEER_DOF[w] >= 0) set(W_SPIN_DOF[w], W_STEER_DOF[w]);
+  }
+  if (kind >= 1) set(EQ_DOF1, EQ_DOF2);
+  if (kind >= 2) {
+    for (int a = 0; a < 6; a++)
+      for (int b = 0; b < 6; b++) set(a, b);
+    for (int w = 0; w < 4; w++)
+      for (int a = 0; a < 6; a++) {
+        set(W_SPIN_DOF[w], a);
+        if (W_STEER_DOF[w] >= 0) set(W_STEER_DOF[w], a);
+      }
+  }
+  return p;
+}
+// pattern of the factor in elimination order (lower triangle, with fill)
+constexpr SymPat make_lpat(int kind) {
+  const SymPat p = make_pat(kind);
+  SymPat l{};
+  for (int i = 0; i < NV; i++)
+    for (int j = 0; j <= i; j++) l.nz[i][j] = p.nz[ORD[i]][ORD[j]];
+  for (int k = 0; k < NV; k++)
+    for (int i = k + 1; i < NV; i++)
+      if (l.nz[i][k])
+        for (int j = k + 1; j <= i; j++)
+          if (l.nz[j][k]) l.nz[i][j] = true;
+  return l;
+}
+constexpr SymPat PAT[4] = {make_pat(0), make_pat(1), make_pat(2), make_pat(3)};
+constexpr SymPat LPAT[4] = {make_lpat(0), make_lpat(1), make_lpat(2), make_lpat(3)};
+constexpr bool no_fill(int kind) {  // the order creates no fill outside the free-joint block
+  for (int i = 0; i < NV; i++)
+    for (int j = 0; j < i; j++)
+      if (LPAT[kind].nz[i][j] && !PAT[kind].nz[ORD[i]][ORD[j]] && (ORD[i] >= 6 || ORD[j] >= 6)) return false;
+  return true;
+}
+static_assert(no_fill(0) && no_fill(1) && no_fill(2), "hinge-first order must not fill hinge rows");
+
+// In-place structured Cholesky: entry (i, j) of the factor in elimination order is stored in the
+// natural lower-triangle slot of dofs (ORD i, ORD j), the diagonal as 1/L_jj. H holds the lower
+// triangle in natural order and is read only where PAT[KIND] is set (fill slots start from 0).
+#define AK_F(A, i, j) A[ORD[i] > ORD[j] ? ORD[i] : ORD[j]][ORD[i] > ORD[j] ? ORD[j] : ORD[i]]
+template <int KIND>
+__device__ __forceinline__ void chol_sp(float H[NV][NV]) {
 #pragma unroll
   for (int j = 0; j < NV; j++) {
-    float s = A[j][j];
+    float s = AK_F(H, j, j);
 #pragma unroll
-    for (int k = 0; k < j; k++) s -= A[j][k] * A[j][k];
-    ok = ok && (s > 0.0f);
-    float inv = __frsqrt_rn(fmaxf(s, 1e-30f));
-    A[j][j] = inv;
+    for (int k = 0; k < j; k++)
+      if (LPAT[KIND].nz[j][k]) s -= AK_F(H, j, k) * AK_F(H, j, k);
+    const float inv = __frsqrt_rn(fmaxf(s, 1e-30f));
+    AK_F(H, j, j) = inv;
 #pragma unroll
     for (int i = j + 1; i < NV; i++) {
-      float t = A[i][j];
+      if (!LPAT[KIND].nz[i][j]) continue;
+      float t = PAT[KIND].nz[ORD[i]][ORD[j]] ? AK_F(H, i, j) : 0.0f;
 #pragma unroll
-      for (int k = 0; k < j; k++) t -= A[i][k] * A[j][k];
-      A[i][j] = t * inv;
+      for (int k = 0; k < j; k++)
+        if (LPAT[KIND].nz[i][k] && LPAT[KIND].nz[j][k]) t -= AK_F(H, i, k) * AK_F(H, j, k);
+      AK_F(H, i, j) = t * inv;
     }
   }
-  return ok;
 }
-__device__ __forceinline__ void chol12_solve(const float L[NV][NV], float x[NV]) {
+// x <- H^-1 x with H factored by chol_sp<KIND>; x in natural dof order
+template <int KIND>
+__device__ __forceinline__ void chol_sp_solve(const float H[NV][NV], float x[NV]) {
+  float y[NV];
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    float s = x[i];
+    float s = x[ORD[i]];
 #pragma unroll
-    for (int k = 0; k < i; k++) s -= L[i][k] * x[k];
-    x[i] = s * L[i][i];
+    for (int k = 0; k < i; k++)
+      if (LPAT[KIND].nz[i][k]) s -= AK_F(H, i, k) * y[k];
+    y[i] = s * AK_F(H, i, i);
   }
 #pragma unroll
   for (int i = NV - 1; i >= 0; i--) {
-    float s = x[i];
+    float s = y[i];
 #pragma unroll
-    for (int k = i + 1; k < NV; k++) s -= L[k][i] * x[k];
-    x[i] = s * L[i][i];
+    for (int k = i + 1; k < NV; k++)
+      if (LPAT[KIND].nz[k][i]) s -= AK_F(H, k, i) * y[k];
+    y[i] = s * AK_F(H, i, i);
   }
+#pragma unroll
+  for (int i = 0; i < NV; i++) x[ORD[i]] = y[i];
 }
-__device__ __forceinline__ void symv12(const float M[NV][NV], const float x[NV], float y[NV]) {
+// y = M x over the mass matrix's structural nonzeros (zero terms skipped, natural summation order)
+template <int KIND = 0>
+__device__ __forceinline__ void symv_M(const float M[NV][NV], const float x[NV], float y[NV]) {
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     float s = 0;
 #pragma unroll
-    for (int j = 0; j < NV; j++) s += (j <= i ? M[i][j] : M[j][i]) * x[j];
+    for (int j = 0; j < NV; j++)
+      if (PAT[KIND].nz[i][j]) s += (j <= i ? M[i][j] : M[j][i]) * x[j];
     y[i] = s;
   }
 }
@@ -717,8 +833,8 @@ __device__ __forceinline__ void slot_loop_init(const Slots& S, const float dirs[
     // pyramidal regulariser shared by the 4 edges:
     // R = (1-imp)/imp * tran*(1+mu^2) * 2 mu^2 / impratio   (see oracle make_constraint)
     float tran = CH < 4 ? W_TRAN[CH < 4 ? CH : 0] : MESH_TRAN[CH >= 4 ? CH - 4 : 0];
-    float Rr = fmaxf(MINVAL, (1.0f - imp) / imp * tran * (1.0f + mu * mu) * (2.0f * mu * mu / IMPRATIO));
-    S.at(s, 3) = 1.0f / Rr;
+    float Rr = fmaxf(MINVAL, fdiv(1.0f - imp, imp) * tran * (1.0f + mu * mu) * (2.0f * mu * mu / IMPRATIO));
+    S.at(s, 3) = frcp(Rr);
   }
 }
 
@@ -763,7 +879,7 @@ __device__ __forceinline__ uint32_t wheel_contacts(const Slots& S, const float p
   float vec[3] = {axis[0] * prjaxis, axis[1] * prjaxis, axis[2] * prjaxis - 1.0f};
   float len2 = dot(vec, vec), prjvec;
   if (len2 >= MINVAL * MINVAL) {
-    float sc = CYL_R / sqrtf(len2);
+    float sc = CYL_R * frsq(len2);
     vec[0] *= sc; vec[1] *= sc; vec[2] *= sc;
     prjvec = vec[2];
   } else {  // disk parallel to the plane (measure zero): any in-plane radius
@@ -789,8 +905,8 @@ __device__ __forceinline__ uint32_t wheel_contacts(const Slots& S, const float p
     if (dist0 + prjaxis - prjvec <= 0.0f) {
       float v1[3];
       cross(v1, vec, axis);
-      float nv1 = sqrtf(dot(v1, v1));
-      float sc = nv1 < MINVAL ? 0.0f : CYL_R * 0.8660254037844386f / nv1;
+      float nv1 = fsqrt(dot(v1, v1));
+      float sc = nv1 < MINVAL ? 0.0f : CYL_R * 0.8660254037844386f * frcp(nv1);
       float d3 = dist0 + prjaxis - 0.5f * prjvec;
 #pragma unroll
       for (int t = 0; t < 2; t++) {
@@ -903,12 +1019,13 @@ __device__ __forceinline__ void euler_advance(const float u[NV], const StepResul
   for (int k = 0; k < 3; k++) qpos[k] += DT * qvel[k];
   {
     const float w[3] = {qvel[3], qvel[4], qvel[5]};
-    const float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const float wn = fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     float ang = DT * wn;
     float ax[3];
     if (wn < MINVAL) { ax[0] = 1; ax[1] = 0; ax[2] = 0; ang = 0; }
-    else { ax[0] = w[0] / wn; ax[1] = w[1] / wn; ax[2] = w[2] / wn; }
-    const float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    else { const float iw = frcp(wn); ax[0] = w[0] * iw; ax[1] = w[1] * iw; ax[2] = w[2] * iw; }
+    float s, c;
+    fsincos(0.5f * ang, s, c);
     const float qr[4] = {c, ax[0] * s, ax[1] * s, ax[2] * s};
     float qq[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
     normq(qq);
@@ -947,7 +1064,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 #pragma unroll
   for (int s = 0; s < 2; s++) {
     float d = qpos[W_STEER_QPOS[2 + s]];
-    float c = cosf(d), sn = sinf(d);
+    float c, sn;
+    fsincos(d, sn, c);
     rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
     rot_axis(cyl[s], S_AXIS[s], W_CYL_AXIS[2 + s], c, sn);
   }
@@ -981,10 +1099,10 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int j = 0; j < NV; j++) L[i][j] = sv.M[i][j];
-  chol12(L);
+  chol_sp<LANE_K(0)>(L);
 #pragma unroll
   for (int i = 0; i < NV; i++) sv.a0[i] = sv.fs[i];
-  chol12_solve(L, sv.a0);
+  chol_sp_solve<LANE_K(0)>(L, sv.a0);
 
   STAMP(3);
   // contacts
@@ -1023,8 +1141,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     float pos = qpos[EQ_QPOS1] - QPOS0[EQ_QPOS1] - cpos;
     float imp = impedance(pos);
     float diag = DOF_INVW[EQ_DOF1] + DOF_INVW[EQ_DOF2];
-    float Rr = fmaxf(MINVAL, (1 - imp) / imp * diag);
-    sD[0] = 1.0f / Rr; sRfl[0] = 0; sfl[0] = 0; sact[0] = true;
+    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * diag);
+    sD[0] = frcp(Rr); sRfl[0] = 0; sfl[0] = 0; sact[0] = true;
     float ja = warm_u[EQ_DOF1] + eqc2 * warm_u[EQ_DOF2];
     float jv = u[EQ_DOF1] + eqc2 * u[EQ_DOF2];
     sj[0] = -B * jv - K * imp * pos;  // holds aref for now
@@ -1034,8 +1152,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   for (int r = 1; r <= 6; r++) {
     int d = 5 + r;
     float imp = impedance(0.0f);
-    float Rr = fmaxf(MINVAL, (1 - imp) / imp * DOF_INVW[d]);
-    sD[r] = 1.0f / Rr; sfl[r] = FRICTIONLOSS[d]; sRfl[r] = Rr * FRICTIONLOSS[d];
+    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[d]);
+    sD[r] = frcp(Rr); sfl[r] = FRICTIONLOSS[d]; sRfl[r] = Rr * FRICTIONLOSS[d];
     sact[r] = FRICTIONLOSS[d] > 0.0f;
     sj[r] = -B * u[d];
   }
@@ -1046,8 +1164,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     float dist = side * (LIM_RANGE[l][side > 0 ? 1 : 0] - q);
     sact[r] = dist < 0.0f;
     float imp = impedance(dist);
-    float Rr = fmaxf(MINVAL, (1 - imp) / imp * DOF_INVW[LIM_DOF[l]]);
-    sD[r] = 1.0f / Rr; sfl[r] = 0; sRfl[r] = 0;
+    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[LIM_DOF[l]]);
+    sD[r] = frcp(Rr); sfl[r] = 0; sRfl[r] = 0;
     float jv = -side * u[LIM_DOF[l]];
     sj[r] = -B * jv - K * imp * dist;
   }
@@ -1076,7 +1194,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     float dw[NV], Mdw[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) dw[i] = warm_u[i] - sv.a0[i];
-    symv12(sv.M, dw, Mdw);
+    symv_M<LANE_K(0)>(sv.M, dw, Mdw);
 #pragma unroll
     for (int i = 0; i < NV; i++) cost_w += 0.5f * dw[i] * Mdw[i];
 #pragma unroll
@@ -1146,7 +1264,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       float da[NV];
 #pragma unroll
       for (int i = 0; i < NV; i++) da[i] = a[i] - sv.a0[i];
-      symv12(sv.M, da, grad);
+      symv_M<LANE_K(0)>(sv.M, da, grad);
 #pragma unroll
       for (int i = 0; i < NV; i++) gscale = fmaxf(gscale, fabsf(grad[i]));
     }
@@ -1184,11 +1302,13 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad);
     (void)gscale;
     NT_MARK(0);
-    chol12(H);
+    if (S.wmask) chol_sp<LANE_K(2)>(H);  // wave-uniform: contact rows present in some lane
+    else chol_sp<LANE_K(1)>(H);
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
-    chol12_solve(H, pdir);
+    if (S.wmask) chol_sp_solve<LANE_K(2)>(H, pdir);
+    else chol_sp_solve<LANE_K(1)>(H, pdir);
     NT_MARK(1);
     // Jp for all rows
     FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir);
@@ -1196,7 +1316,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     for (int r = 0; r < NSCAL; r++) sjp[r] = scal_J_dot(r, pdir);
     // exact line search on the piecewise-linear derivative phi'(alpha)
     float Mp[NV];
-    symv12(sv.M, pdir, Mp);
+    symv_M<LANE_K(0)>(sv.M, pdir, Mp);
     float pMp = 0.0f, pg0 = 0.0f;
 #pragma unroll
     for (int i = 0; i < NV; i++) { pMp += pdir[i] * Mp[i]; pg0 += Mp[i] * (a[i] - sv.a0[i]); }
@@ -1316,10 +1436,10 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     for (int j = 0; j < NV; j++) L[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
 #pragma unroll
   for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
-  chol12(L);
+  chol_sp<LANE_K(0)>(L);
 #pragma unroll
   for (int i = 0; i < NV; i++) out.acce[i] = sv.fs[i] + fc[i];
-  chol12_solve(L, out.acce);
+  chol_sp_solve<LANE_K(0)>(L, out.acce);
   bool bad = false;
 #pragma unroll
   for (int i = 0; i < NV; i++) bad |= is_bad(a[i]);

@@ -93,12 +93,30 @@ def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
 
 
 def test_contact_boundary_state_is_excused(blob):
-    """The recorded boundary case: both step kernels put the second plate vertex (dist ~0) in
-    contact; the f64 oracle does not, but does once the body is lowered by 1e-7 m."""
+    """The recorded boundary case: a second plate vertex at dist ~0 whose contact activation depends
+    on the last bits (the f32 kernels have put it in contact where the f64 oracle does not; which
+    side a kernel lands on moves with its rounding). Each kernel's step must match the oracle or be
+    excused; the excuse itself is checked independently of the kernels' rounding: the boundary is
+    genuine (a 1e-7 m shift changes the oracle's step beyond the tolerances), the shifted step is
+    excused, a wrong step is not."""
     d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
                                            "quad_miss_state.npz"))
     before, action = d["before"], d["action"].astype(np.float32)
     o = fresh_oracle(blob)
+    ref = before[None].copy()
+    o.step(ref, action[None], flags=3, seed=11)
+    shifted = []
+    for dz in BOUNDARY_DZ:
+        s = before[None].copy()
+        s[0, 2] += dz
+        o.step(s, action[None], flags=3, seed=11)
+        shifted.append(s[0])
+    far = max(shifted, key=lambda s: np.abs(s[:13] - ref[0, :13]).max())
+    assert np.abs(far[:13] - ref[0, :13]).max() > TOL_QPOS  # a 1e-7..1e-6 m shift flips the contact set
+    assert _boundary_excused(o, before, action, far, 3, 11)
+    wrong = ref[0].copy()
+    wrong[13] += 0.1
+    assert not _boundary_excused(o, before, action, wrong, 3, 11)
     for variant in ("lane", "quad"):
         sim = make_sim(1, seed=11, contacts=True, variant=variant)
         st = before[:, None].astype(np.float32)
@@ -107,10 +125,9 @@ def test_contact_boundary_state_is_excused(blob):
         sim.step(torch.tensor(action[None], device=DEV))
         torch.cuda.synchronize()
         after = f64_state(sim.state)[0]
-        ref = before[None].copy()
-        o.step(ref, action[None], flags=3, seed=11)
-        assert np.abs(after[:13] - ref[0, :13]).max() > TOL_QPOS  # a genuine boundary miss ...
-        assert _boundary_excused(o, before, action, after, 3, 11)  # ... explained by a 1e-7 m shift
+        match = (np.abs(after[:13] - ref[0, :13]).max() <= TOL_QPOS and
+                 np.abs(after[13:25] - ref[0, 13:25]).max() <= TOL_QVEL)
+        assert match or _boundary_excused(o, before, action, after, 3, 11), variant
 
 
 def test_reset_matches_oracle(blob):
