@@ -1507,11 +1507,9 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
 // ====================================================================== kernels
 using namespace ak;
 
-extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) {
-  __shared__ float lds[NSLOT * NF * 64];
-  const int lane = threadIdx.x;
-  const int e = blockIdx.x * A.epw + lane;
-  if (lane >= A.epw || e >= A.n) return;
+// The whole step of one env on one lane, observation included (F_POSTSTEP_OBS: obs/reward need the
+// integrated pose, so nothing can run beside the dynamics).
+__device__ __forceinline__ void step_serial(const Args& A, float* lds, int lane, int e) {
   const int n = A.n;
   STAMP(0);
   Slots S{lds + lane};
@@ -1622,6 +1620,187 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_kernel(Args A) 
     STAMP(10);
     return;
   }
+}
+
+// Wave-specialised step (default flags): a 128-lane workgroup holds 64 envs twice. Wave 0 runs the
+// dynamics (controller, Newton, Euler) and writes the state; wave 1, on another SIMD of the CU, runs
+// the observation of the same envs -- odometry, the 72 rays, reward, done flags, Monitor stats --
+// which mj_step takes at the PRE-integration pose (a10-a13), so it needs nothing from wave 0 except
+// in two places, exchanged through LDS at two barriers:
+//   barrier 1: wave 0 -> wave 1 "this env's dynamics blew up" (mj_checkAcc -> mj_resetData: the
+//              step is redone from qpos0, so its observation is taken at qpos0 too; rare);
+//   barrier 2: wave 1 -> wave 0 "auto-reset this env" (term from the goal distance, trunc), after
+//              wave 1 has written obs, so wave 0's reset observation lands last.
+// The observation leaves the critical path (~20 % of the serial step).
+__device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t* sh_bad, const uint8_t* sh_reset,
+                                              int lane, int e, bool valid) {
+  const int n = A.n;
+  Slots S{lds + lane};
+  const uint32_t vo = 4u * (uint32_t)e;
+  const Soa st = soa(A.state, NSTATE, n);
+  float qpos[13], qvel[NV], warm[NV];
+  bool redo = false;
+  uint32_t step = 0, episode = 0;
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+#pragma unroll
+    for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
+    step = __float_as_uint(ldf(st, ST_STEP, vo));
+    episode = __float_as_uint(ldf(st, ST_EPIS, vo));
+    const Soa act = soa(A.action, 2, n);
+    const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+    float ctrl[3];
+    bool badctrl;
+    controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    bool bad_state = false;
+#pragma unroll
+    for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
+#pragma unroll
+    for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
+#pragma unroll 1
+    for (int pass = 0; pass < 2; pass++) {
+      if (bad_state) {
+#pragma unroll
+        for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+#pragma unroll
+        for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
+        ctrl[0] = ctrl[1] = ctrl[2] = 0.0f;
+      }
+      float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+      normq(q);
+      float R[9];
+      quat_R(q, R);
+      float u[NV], wu[NV];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        u[k] = R[k] * qvel[0] + R[3 + k] * qvel[1] + R[6 + k] * qvel[2];
+        wu[k] = R[k] * warm[0] + R[3 + k] * warm[1] + R[6 + k] * warm[2];
+      }
+#pragma unroll
+      for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
+      StepResult res;
+      dynamics(S, qpos, u, wu, R, ctrl, A.flags, res);
+      if (res.bad && pass == 0) { bad_state = true; redo = true; continue; }
+      euler_advance(u, res, R, qpos, qvel, warm);
+      break;
+    }
+  }
+  sh_bad[lane] = redo ? 1 : 0;
+  __syncthreads();  // 1: wave 1 learns which envs were redone from qpos0
+  __syncthreads();  // 2: wave 1 has written obs/reward/flags and decided the auto-resets
+  if (!valid) return;
+  if (sh_reset[lane]) {
+    reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 13; i++) stf(st, ST_QPOS + i, vo, qpos[i]);
+#pragma unroll
+  for (int i = 0; i < NV; i++) stf(st, ST_QVEL + i, vo, qvel[i]);
+#pragma unroll
+  for (int i = 0; i < NV; i++) stf(st, ST_WARM + i, vo, warm[i]);
+  stf(st, ST_STEP, vo, __uint_as_float(step + 1));
+}
+
+__device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
+                                              bool valid) {
+  const int n = A.n;
+  const uint32_t vo = 4u * (uint32_t)e;
+  const Soa st = soa(A.state, NSTATE, n);
+  const Soa obs = soa(A.obs, NOBS, n);
+  float qpos[7];
+  float gx = 0.0f, gy = 0.0f, ref[3] = {0.0f, 0.0f, 0.0f};
+  uint32_t step = 0;
+  bool bad_state = false;
+  float ep0 = 0.0f, ep1 = 0.0f, ep2 = 0.0f, ep3 = 0.0f;
+  const Soa ep = soa(A.ep, 4, n);
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+    gx = ldf(st, ST_GOAL, vo);
+    gy = ldf(st, ST_GOAL + 1, vo);
+#pragma unroll
+    for (int k = 0; k < 3; k++) ref[k] = ldf(st, ST_REF + k, vo);
+    step = __float_as_uint(ldf(st, ST_STEP, vo));
+    if (A.ep) { ep0 = ldf(ep, 0, vo); ep1 = ldf(ep, 1, vo); ep2 = ldf(ep, 2, vo); ep3 = ldf(ep, 3, vo); }
+    // mj_checkPos / mj_checkVel on the loaded state (the same test as wave 0's)
+#pragma unroll
+    for (int i = 0; i < 13; i++) bad_state |= is_bad(ldf(st, ST_QPOS + i, vo));
+#pragma unroll
+    for (int i = 0; i < NV; i++) bad_state |= is_bad(ldf(st, ST_QVEL + i, vo));
+  }
+  const uint32_t nstep = step + 1;
+  const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
+  ObsOut o{};
+  bool redo = false;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    if (bad_state || redo) {
+#pragma unroll
+      for (int i = 0; i < 7; i++) qpos[i] = QPOS0[i];
+    }
+    if (valid && (pass == 0 || redo)) {
+      float p[3] = {qpos[0], qpos[1], qpos[2]};
+      float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+      normq(q);
+      float R[9];
+      quat_R(q, R);
+      o = observe<0>(p, q, R, gx, gy, ref, obs, vo, A.prm);
+      stf(soa(A.reward, 1, n), 0, vo, o.reward);
+      stb(soa(A.term, 1, n, 1), (uint32_t)e, o.term ? 1 : 0);
+      stb(soa(A.trunc, 1, n, 1), (uint32_t)e, trunc ? 1 : 0);
+      if (A.info) {
+        const Soa inf = soa(A.info, 4, n);
+        stf(inf, 0, vo, o.minl);
+        stf(inf, 1, vo, o.coll ? 1.0f : 0.0f);
+        stf(inf, 2, vo, o.dist);
+        stf(inf, 3, vo, (bad_state || redo) ? 1.0f : 0.0f);
+      }
+    }
+    if (pass == 1) break;
+    __syncthreads();  // 1
+    redo = valid && sh_bad[lane];
+    if (__builtin_amdgcn_ballot_w64(redo) == 0ull) break;
+  }
+  const bool autoreset = valid && (A.flags & F_AUTORESET) && (o.term || trunc);
+  if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset);
+  if (valid && A.ep) {
+    // Monitor-wrapper episode bookkeeping (train.py:70): r/l of finished episodes
+    float ret = ep0 + o.reward, len = ep1 + 1.0f;
+    if (o.term || trunc) {
+      stf(ep, 2, vo, ep2 + ret);
+      stf(ep, 3, vo, ep3 + 1.0f);
+      ret = 0.0f;
+      len = 0.0f;
+    }
+    stf(ep, 0, vo, ret);
+    stf(ep, 1, vo, len);
+  }
+  sh_reset[lane] = autoreset ? 1 : 0;
+  __syncthreads();  // 2
+}
+
+// F_POSTSTEP_OBS (render_mode="human"): one lane per env runs the whole step
+extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(Args A) {
+  __shared__ float lds[NSLOT * NF * 64];
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * A.epw + lane;
+  if (lane >= A.epw || e >= A.n) return;
+  step_serial(A, lds, lane, e);
+}
+
+extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) {
+  __shared__ float lds[NSLOT * NF * 64];
+  __shared__ uint8_t sh_bad[64], sh_reset[64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * A.epw + lane;
+  const bool valid = lane < A.epw && e < A.n;
+  if (wave == 0) step_dyn_wave(A, lds, sh_bad, sh_reset, lane, e, valid);
+  else step_obs_wave(A, sh_bad, sh_reset, lane, e, valid);
 }
 
 template <int SC>
@@ -1788,7 +1967,10 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
   } else {
     a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
     int blocks = (ctx->n_env + a.epw - 1) / a.epw;
-    hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    if (flags & ACKPHYS_POSTSTEP_OBS)
+      hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");

@@ -168,17 +168,22 @@ def test_poststep_obs_mode(blob, variant):
     teacher_forced(sim, fresh_oracle(blob, max_episode_steps=30), acts, steps, 1 | 2 | 4, seed)
 
 
-def test_autoreset_truncation_terminal_obs(blob):
+MAPPINGS = [("quad", True), ("lane", True), ("lane", False), ("lane16", False)]
+
+
+@pytest.mark.parametrize("variant,contacts", MAPPINGS)
+def test_autoreset_truncation_terminal_obs(blob, variant, contacts):
     n, seed = 64, 3
-    sim = make_sim(n, seed=seed, max_episode_steps=25)
+    sim = make_sim(n, seed=seed, max_episode_steps=25, variant=variant, contacts=contacts)
     sim.reset()
     acts = sim.random_actions(60, seed=seed)
     o = fresh_oracle(blob, max_episode_steps=25)
     st = f64_state(sim.state)
+    flags = 2 | (1 if contacts else 0)
     for k in range(60):
         sim.step(acts[k])
         torch.cuda.synchronize()
-        oobs, orew, oterm, otr, tobs, _ = o.step(st, acts[k].cpu().numpy(), flags=3, seed=seed, terminal=True)
+        oobs, orew, oterm, otr, tobs, _ = o.step(st, acts[k].cpu().numpy(), flags=flags, seed=seed, terminal=True)
         g = f64_state(sim.state)
         done = oterm | otr
         assert np.array_equal(sim.trunc.cpu().numpy().astype(bool), otr)
@@ -235,17 +240,46 @@ def test_bad_ctrl_nan_path(blob):
     teacher_forced(sim, fresh_oracle(blob), acts, 5, 3, seed)
 
 
-def test_bad_state_resets(blob):
+@pytest.mark.parametrize("variant,contacts", MAPPINGS)
+def test_bad_state_resets(blob, variant, contacts):
     n, seed = 64, 4
-    sim = make_sim(n, seed=seed)
+    sim = make_sim(n, seed=seed, variant=variant, contacts=contacts)
     sim.reset()
     st = sim.state.clone()
     st[13, :8] = float("nan")          # bad qvel
     st[0, 8:16] = 3e10                  # bad qpos
     sim.set_state(st)
     acts = sim.random_actions(3, seed=seed)
-    teacher_forced(sim, fresh_oracle(blob), acts, 3, 3, seed)
+    teacher_forced(sim, fresh_oracle(blob), acts, 3, 2 | (1 if contacts else 0), seed)
     assert torch.isfinite(sim.state).all()
+
+
+@pytest.mark.parametrize("variant,contacts", MAPPINGS)
+def test_bad_acceleration_redo(blob, variant, contacts):
+    """mj_checkAcc: a finite state whose accelerations blow up (hinge speeds 1e6 rad/s) is reset to
+    qpos0 and the step redone from there -- dynamics, observation (taken at qpos0), reward, info[3]."""
+    n, seed = 64, 6
+    sim = make_sim(n, seed=seed, variant=variant, contacts=contacts)
+    sim.reset()
+    acts = sim.random_actions(4, seed=seed)
+    o = fresh_oracle(blob)
+    flags = 2 | (1 if contacts else 0)
+    teacher_forced(sim, o, acts[:1], 1, flags, seed)
+    st = sim.state.clone()
+    st[13 + 6:13 + 12, ::3] = 1e6      # every third env: hinge speeds that trip mj_checkAcc
+    sim.set_state(st)
+    before = f64_state(sim.state)
+    sim.step(acts[1])
+    torch.cuda.synchronize()
+    ref = before.copy()
+    oobs, orew, oterm, otr, _, oinfo = o.step(ref, acts[1].cpu().numpy(), flags=flags, seed=seed, terminal=True)
+    after = f64_state(sim.state)
+    assert np.abs(after[:, :25] - ref[:, :25]).max() <= TOL_QVEL
+    np.testing.assert_allclose(sim.obs_soa.cpu().numpy().T, oobs, atol=TOL_OBS)
+    np.testing.assert_allclose(sim.reward.cpu().numpy(), orew, atol=TOL_REW)
+    np.testing.assert_array_equal(sim.info[3].cpu().numpy(), oinfo[:, 3])
+    assert oinfo[::3, 3].all() and not oinfo[1::3, 3].any()
+    teacher_forced(sim, o, acts[2:], 2, flags, seed)
 
 
 @pytest.mark.parametrize("variant", ["quad", "lane"])
