@@ -1960,10 +1960,16 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     if (ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
       return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
     int blocks = (ctx->n_env + 15) / 16;
-    hipLaunchKernelGGL(ackphys_step_obst_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    if (flags & ACKPHYS_POSTSTEP_OBS)
+      hipLaunchKernelGGL(ackphys_step_obst_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(ackphys_step_obst_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   } else if (quad) {
     int blocks = (ctx->n_env + 15) / 16;
-    hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    if (flags & ACKPHYS_POSTSTEP_OBS)
+      hipLaunchKernelGGL(ackphys_step_quad_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   } else {
     a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
     int blocks = (ctx->n_env + a.epw - 1) / a.epw;
