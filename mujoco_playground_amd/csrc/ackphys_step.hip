@@ -1057,6 +1057,7 @@ __device__ __forceinline__ void obs_pose(uint32_t flags, const float qpos[13], f
 }
 
 // forward dynamics + constraint solve for one env (state in registers), u coordinates
+template <int NC>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
 __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
                          const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
   // front steer angles -> spin / cylinder axes in the chassis frame
@@ -1107,7 +1108,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   STAMP(3);
   // contacts
   S.lmask = 0u;
-  if (flags & F_CONTACTS) {
+  if (!NC && (flags & F_CONTACTS)) {
     const float rear_cyl[3] = {W_CYL_AXIS[0][0], W_CYL_AXIS[0][1], W_CYL_AXIS[0][2]};
     const float rear_cyl1[3] = {W_CYL_AXIS[1][0], W_CYL_AXIS[1][1], W_CYL_AXIS[1][2]};
     S.lmask |= wheel_contacts<0>(S, qpos, R, rear_cyl);
@@ -1119,9 +1120,12 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   }
   // wave-uniform union of active slots (24 ballots -> SGPR mask)
   S.wmask = 0u;
+  if constexpr (!NC) {
 #pragma unroll
-  for (int b = 0; b < NSLOT; b++)
-    if (__ballot((S.lmask >> b) & 1u)) S.wmask |= 1u << b;
+    for (int b = 0; b < NSLOT; b++)
+      if (__ballot((S.lmask >> b) & 1u)) S.wmask |= 1u << b;
+  }
+  const uint32_t wm = NC ? 0u : S.wmask;  // compile-time 0 without contacts: every slot loop folds away
   // contact frame directions in the chassis frame: n = e_z, t1 = e_y, t2 = -e_x (mju_makeFrame)
   float dirs[3][3] = {{R[6], R[7], R[8]}, {R[3], R[4], R[5]}, {-R[0], -R[1], -R[2]}};
 
@@ -1205,9 +1209,9 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   }
   // contact rows: need jar at both candidates. Initialise slots at warm and at a0 (cheap).
   // slot field 4..7 temporarily = J a_w - aref ; we evaluate cost then re-init for the chosen.
-  FOR_CHAINS(slot_loop_init, S, dirs, sa, warm_u, u, K, B);
+  if constexpr (!NC) { FOR_CHAINS(slot_loop_init, S, dirs, sa, warm_u, u, K, B); }
   float cw_c = 0.0f;
-  FOR_SLOTS(S, S.wmask, s) {
+  FOR_SLOTS(S, wm, s) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       float x = S.at(s, 4 + r);
@@ -1221,9 +1225,9 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     float dpa[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) dpa[i] = sv.a0[i] - warm_u[i];
-    FOR_CHAINS(slot_loop_jp, S, dirs, sa, dpa);
+    if constexpr (!NC) { FOR_CHAINS(slot_loop_jp, S, dirs, sa, dpa); }
     float cs_c = 0.0f;
-    FOR_SLOTS(S, S.wmask, s) {
+    FOR_SLOTS(S, wm, s) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         float x = S.at(s, 4 + r) + S.at(s, 8 + r);
@@ -1235,7 +1239,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = use_w ? warm_u[i] : sv.a0[i];
     if (!use_w) {
-      FOR_SLOTS(S, S.wmask, s) {
+      FOR_SLOTS(S, wm, s) {
 #pragma unroll
         for (int r = 0; r < 4; r++) S.at(s, 4 + r) += S.at(s, 8 + r);
       }
@@ -1299,19 +1303,19 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
         }
       }
     }
-    FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad);
+    if constexpr (!NC) { FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad); }
     (void)gscale;
     NT_MARK(0);
-    if (S.wmask) chol_sp<LANE_K(2)>(H);  // wave-uniform: contact rows present in some lane
+    if (wm) chol_sp<LANE_K(2)>(H);  // wave-uniform: contact rows present in some lane
     else chol_sp<LANE_K(1)>(H);
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
-    if (S.wmask) chol_sp_solve<LANE_K(2)>(H, pdir);
+    if (wm) chol_sp_solve<LANE_K(2)>(H, pdir);
     else chol_sp_solve<LANE_K(1)>(H, pdir);
     NT_MARK(1);
     // Jp for all rows
-    FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir);
+    if constexpr (!NC) { FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir); }
 #pragma unroll
     for (int r = 0; r < NSCAL; r++) sjp[r] = scal_J_dot(r, pdir);
     // exact line search on the piecewise-linear derivative phi'(alpha)
@@ -1324,7 +1328,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       g = fmaf(al, pMp, pg0);
       h = pMp;
       scal_ls<0>(al, sj, sjp, sD, sRfl, sfl, sact, 0, g, h);
-      FOR_SLOTS(S, S.wmask, s) {
+      FOR_SLOTS(S, wm, s) {
         float D = S.at(s, 3);
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -1340,7 +1344,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     for (int i = 0; i < NV; i++) g0 += grad[i] * pdir[i];
     if (!(g0 < 0.0f)) { it_done = it; why = 3; break; }  // no descent left: optimum to f32 precision
     float ns = fabsf(pg0) + fabsf(pMp) + scal_noise<0>(sj, sjp, sD, sRfl, sfl, sact, 0);
-    FOR_SLOTS(S, S.wmask, s) {
+    FOR_SLOTS(S, wm, s) {
       const float D = S.at(s, 3);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -1383,7 +1387,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       }
       sj[r] = x1;
     }
-    FOR_SLOTS(S, S.wmask, s) {
+    FOR_SLOTS(S, wm, s) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         float x0 = S.at(s, 4 + r), x1 = x0 + al * S.at(s, 8 + r);
@@ -1428,7 +1432,7 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
     fc[d1] += f * c1;
     if (d2 >= 0) fc[d2] += f * eqc2;
   }
-  FOR_CHAINS(slot_loop_force, S, dirs, sa, fc);
+  if constexpr (!NC) { FOR_CHAINS(slot_loop_force, S, dirs, sa, fc); }
   // implicit damping Euler: (M + h diag(B)) acc = fs + fc
 #pragma unroll
   for (int i = 0; i < NV; i++)
@@ -1565,7 +1569,7 @@ __device__ __forceinline__ void step_serial(const Args& A, float* lds, int lane,
 #pragma unroll
     for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
     StepResult res;
-    dynamics(S, qpos, u, wu, R, ctrl, A.flags, res);
+    dynamics<0>(S, qpos, u, wu, R, ctrl, A.flags, res);
     if (res.bad && pass == 0) { bad_state = true; continue; }
 
     STAMP(8);
@@ -1632,6 +1636,7 @@ __device__ __forceinline__ void step_serial(const Args& A, float* lds, int lane,
 //   barrier 2: wave 1 -> wave 0 "auto-reset this env" (term from the goal distance, trunc), after
 //              wave 1 has written obs, so wave 0's reset observation lands last.
 // The observation leaves the critical path (~20 % of the serial step).
+template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t* sh_bad, const uint8_t* sh_reset,
                                               int lane, int e, bool valid) {
   const int n = A.n;
@@ -1682,7 +1687,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
 #pragma unroll
       for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
       StepResult res;
-      dynamics(S, qpos, u, wu, R, ctrl, A.flags, res);
+      dynamics<NC>(S, qpos, u, wu, R, ctrl, A.flags, res);
       if (res.bad && pass == 0) { bad_state = true; redo = true; continue; }
       euler_advance(u, res, R, qpos, qvel, warm);
       break;
@@ -1792,16 +1797,20 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
   step_serial(A, lds, lane, e);
 }
 
-extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) {
-  __shared__ float lds[NSLOT * NF * 64];
+template <int NC>
+__device__ __forceinline__ void step_split(const Args& A) {
+  __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
   __shared__ uint8_t sh_bad[64], sh_reset[64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * A.epw + lane;
   const bool valid = lane < A.epw && e < A.n;
-  if (wave == 0) step_dyn_wave(A, lds, sh_bad, sh_reset, lane, e, valid);
+  if (wave == 0) step_dyn_wave<NC>(A, lds, sh_bad, sh_reset, lane, e, valid);
   else step_obs_wave(A, sh_bad, sh_reset, lane, e, valid);
 }
+extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) { step_split<0>(A); }
+// contacts off (BASELINE configs[1]): the contact machinery is compiled out
+extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_nc_kernel(Args A) { step_split<1>(A); }
 
 template <int SC>
 __device__ __forceinline__ void reset_body(const uint8_t* mask, float* state, float* obs, int n, uint64_t seed,
@@ -1975,8 +1984,10 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
-    else
+    else if (flags & ACKPHYS_CONTACTS)
       hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");

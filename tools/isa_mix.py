@@ -12,7 +12,7 @@ from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "mujoco_playground_amd", "csrc", "ackphys_step.hip")
-KERNELS = ["ackphys_step_kernel", "ackphys_step_serial_kernel", "ackphys_step_quad_serial_kernel", "ackphys_step_quad_kernel", "ackphys_step_obst_kernel"]
+KERNELS = ["ackphys_step_kernel", "ackphys_step_nc_kernel", "ackphys_step_serial_kernel", "ackphys_step_quad_serial_kernel", "ackphys_step_quad_kernel", "ackphys_step_obst_kernel"]
 
 
 def category(op: str) -> str:
