@@ -359,6 +359,9 @@ struct SymPat { bool nz[NV][NV]; };
 #define AK_QUAD_DENSE 1  // measured: dense 90.2 us vs structured 95.5 us per contacts-on step
 #endif
 #define LANE_K(k) (AK_LANE_DENSE ? 3 : (k))
+#ifndef AK_NC_WARMSTART
+#define AK_NC_WARMSTART 1  // contacts-off kernel: Newton starts from qacc_warmstart (see dynamics())
+#endif
 #define QUAD_K(k) (AK_QUAD_DENSE ? 3 : (k))
 #ifdef AK_ORD_IDENT
 constexpr int ORD[NV] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
@@ -1235,7 +1238,14 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       }
     }
     cost_s += cs_c;
-    bool use_w = cost_w < cost_s;
+    // Newton start. MuJoCo takes the cheaper of qacc_warmstart and qacc_smooth; the contacts-off
+    // kernel starts from qacc_warmstart (AK_NC_WARMSTART): the cost is strictly convex (M > 0), so
+    // both starts reach the same unique minimiser -- the parity tests hold it to the oracle, which
+    // applies MuJoCo's rule -- and on the benchmark workload the oracle's rule picks qacc_smooth
+    // for 85 % of env-steps, from where Newton needs one more iteration (wave max 3 vs 2). With
+    // contacts (stiff, ill-conditioned in f32) the f32 solve's last digits depend on the start, so
+    // the contact kernels keep MuJoCo's rule.
+    const bool use_w = (NC && AK_NC_WARMSTART) ? true : cost_w < cost_s;
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = use_w ? warm_u[i] : sv.a0[i];
     if (!use_w) {
@@ -1647,6 +1657,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
   bool redo = false;
   uint32_t step = 0, episode = 0;
   if (valid) {
+    STAMP(0);
 #pragma unroll
     for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
 #pragma unroll
@@ -1660,6 +1671,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
     float ctrl[3];
     bool badctrl;
     controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    STAMP(1);
     bool bad_state = false;
 #pragma unroll
     for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
@@ -1690,13 +1702,17 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
       dynamics<NC>(S, qpos, u, wu, R, ctrl, A.flags, res);
       if (res.bad && pass == 0) { bad_state = true; redo = true; continue; }
       euler_advance(u, res, R, qpos, qvel, warm);
+      STAMP(8);
       break;
     }
   }
   sh_bad[lane] = redo ? 1 : 0;
-  __syncthreads();  // 1: wave 1 learns which envs were redone from qpos0
-  __syncthreads();  // 2: wave 1 has written obs/reward/flags and decided the auto-resets
+  __syncthreads();  // 1: wave 1 has written obs and the auto-reset decisions; it learns the redos
+  // 2 (only when some env of the workgroup was redone; both waves read the same 64 bytes): wave 1
+  // has re-observed the redone envs at qpos0 and revised their auto-reset decisions
+  if (__builtin_amdgcn_ballot_w64(sh_bad[lane] != 0) != 0ull) __syncthreads();
   if (!valid) return;
+  STAMP(9);
   if (sh_reset[lane]) {
     reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm);
     return;
@@ -1708,6 +1724,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
 #pragma unroll
   for (int i = 0; i < NV; i++) stf(st, ST_WARM + i, vo, warm[i]);
   stf(st, ST_STEP, vo, __uint_as_float(step + 1));
+  STAMP(10);
 }
 
 __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
@@ -1740,7 +1757,7 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
   const uint32_t nstep = step + 1;
   const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
   ObsOut o{};
-  bool redo = false;
+  bool redo = false, autoreset = false;
 #pragma unroll 1
   for (int pass = 0; pass < 2; pass++) {
     if (bad_state || redo) {
@@ -1764,14 +1781,16 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
         stf(inf, 2, vo, o.dist);
         stf(inf, 3, vo, (bad_state || redo) ? 1.0f : 0.0f);
       }
+      autoreset = (A.flags & F_AUTORESET) && (o.term || trunc);
     }
+    // terminal obs before wave 0 may overwrite obs with the reset observation
+    if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset && (pass == 0 || redo));
+    sh_reset[lane] = autoreset ? 1 : 0;
+    __syncthreads();  // pass 0: barrier 1; pass 1: barrier 2 (see step_dyn_wave)
     if (pass == 1) break;
-    __syncthreads();  // 1
+    if (__builtin_amdgcn_ballot_w64(sh_bad[lane] != 0) == 0ull) break;
     redo = valid && sh_bad[lane];
-    if (__builtin_amdgcn_ballot_w64(redo) == 0ull) break;
   }
-  const bool autoreset = valid && (A.flags & F_AUTORESET) && (o.term || trunc);
-  if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset);
   if (valid && A.ep) {
     // Monitor-wrapper episode bookkeeping (train.py:70): r/l of finished episodes
     float ret = ep0 + o.reward, len = ep1 + 1.0f;
@@ -1784,8 +1803,6 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
     stf(ep, 0, vo, ret);
     stf(ep, 1, vo, len);
   }
-  sh_reset[lane] = autoreset ? 1 : 0;
-  __syncthreads();  // 2
 }
 
 // F_POSTSTEP_OBS (render_mode="human"): one lane per env runs the whole step

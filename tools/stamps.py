@@ -16,9 +16,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 # (from stamp, to stamp, name): the kernel's stamps in execution order
-PHASES = [(0, 1, "controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3, 4, "contacts"), (4, 5, "rows+warm"),
-          (5, 6, "newton"), (6, 7, "force+euler"), (7, 8, "->obs"), (8, 11, "obs head (+euler)"),
-          (11, 12, "rays"), (12, 9, "obs stores+reward"), (9, 10, "state store")]
+PHASES = [(0, 1, "load+controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3, 4, "contacts"),
+          (4, 5, "rows+warm"), (5, 6, "newton"), (6, 7, "force+euler solve"), (7, 8, "integrate"),
+          (8, 9, "barriers"), (9, 10, "state store"), (11, 12, "obs wave: rays")]
 
 
 QUAD_PHASES = [(0, 5, "pre-newton"), (5, 6, "newton"), (6, 10, "post-newton")]
@@ -60,7 +60,7 @@ def main():
             L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
                            stream)
         torch.cuda.synchronize()
-        res = []
+        res, spans = [], []
         for k in range(200, 210):
             stamps.zero_()
             L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
@@ -69,6 +69,7 @@ def main():
             allv = stamps.cpu().numpy()
             s = allv[: 16 * nb].reshape(16, nb)
             res.append(np.stack([s[b] - s[a] for a, b, _ in phases]))
+            spans.append(s[10] - s[0] if not quad else np.sum(res[-1], axis=0))
             its = allv[16 * nb:16 * nb + 64 * nb]
             nt = allv[16 * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
@@ -84,7 +85,7 @@ def main():
                       f"wave-max hist {np.bincount(wmax, minlength=13)}, exit reasons (1 exact,2 grad,3 nodesc,4 maxit) "
                       f"{np.bincount(why, minlength=5)[1:]}")
         d = np.median(np.concatenate(res, axis=1), axis=1)
-        tot = np.median(np.concatenate([np.sum(r, axis=0) for r in res]))
+        tot = np.median(np.concatenate(spans))
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
         for (_, _, name), v in zip(phases, d):
             print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
