@@ -255,7 +255,7 @@ def main():
     bpe = algorithmic_bytes_per_env_step()
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
     kern = "ackphys_step_quad_kernel" if (a.variant == "quad" or (a.variant == "auto" and contacts)) \
-        else "ackphys_step_kernel"
+        else ("ackphys_step_kernel" if contacts else "ackphys_step_nc_kernel")
     pmc = load_pmc(kern, contacts)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     valu = None
@@ -264,7 +264,8 @@ def main():
         valu = {"insts_per_wave": pmc["valu_insts_per_wave"], "waves": pmc["SQ_WAVES"],
                 "issue_frac_of_kernel_time": pmc["valu_insts_per_wave"] * 4 / (kern_ms * 1e-3 * 2.4e9),
                 "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave rate "
-                        "(4 cyc/op, 2.4 GHz); the rest is dependency/memory latency"}
+                        "(4 cyc/op, 2.4 GHz), per-wave average over the dynamics and observation waves; the "
+                        "rest is dependency/memory latency"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -279,7 +280,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kern_ms, "valu": valu,
                          "algorithmic_bytes_per_env_step": bpe,
-                         "note": "latency/VALU-bound at 64 waves per 4096 envs; HBM fraction is tiny by construction"},
+                         "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation waves (lane "
+                                 "mapping), i.e. 128 of 1024 SIMDs; HBM fraction is tiny by construction"},
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
             "obstacles": obstacles,
         }

@@ -1,6 +1,6 @@
 """rocprofv3 PMC passes for the step kernels -> gpurun_out/pmc_latest.json (run on the GPU box).
 
-For each workload (contacts off -> ackphys_step_kernel, contacts on -> ackphys_step_quad_kernel,
+For each workload (contacts off -> ackphys_step_nc_kernel, contacts on -> ackphys_step_quad_kernel,
 the kernels bench.py's AUTO mapping runs) three separate passes, kernel-trace only, no
 sys/runtime trace:
   FETCH_SIZE, WRITE_SIZE (HBM bytes; they do not fit one TCC pass on gfx950),
@@ -17,7 +17,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {0: "ackphys_step_kernel", 1: "ackphys_step_quad_kernel"}
+KERNELS = {0: "ackphys_step_nc_kernel", 1: "ackphys_step_quad_kernel"}
 
 
 def run_pass(counters, out, contacts):

@@ -14,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SQ = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
       "SQ_INSTS_VALU", "SQ_INSTS_SALU"]
-RUNS = [("lane_off", "ackphys_step_kernel", ["--contacts", "0", "--variant", "lane"]),
+RUNS = [("lane_off", "ackphys_step_nc_kernel", ["--contacts", "0", "--variant", "lane"]),
         ("quad_on", "ackphys_step_quad_kernel", ["--contacts", "1", "--variant", "quad"])]
 
 
