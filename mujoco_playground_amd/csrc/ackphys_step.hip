@@ -359,6 +359,9 @@ struct SymPat { bool nz[NV][NV]; };
 #define AK_QUAD_DENSE 1  // measured: dense 90.2 us vs structured 95.5 us per contacts-on step
 #endif
 #define LANE_K(k) (AK_LANE_DENSE ? 3 : (k))
+#ifndef AK_QUAD_START
+#define AK_QUAD_START 1  // quad kernels: Newton from qacc_smooth (0 = MuJoCo's start rule), see dynamics_quad()
+#endif
 #ifndef AK_NC_WARMSTART
 #define AK_NC_WARMSTART 1  // contacts-off kernel: Newton starts from qacc_warmstart (see dynamics())
 #endif

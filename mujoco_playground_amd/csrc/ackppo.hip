@@ -157,12 +157,18 @@ struct ActArgs {
   float* value;
 };
 
-// Policy tile: 64 envs (lane = env) x 4 waves. The whole parameter vector is staged in LDS once
-// per workgroup (wide coalesced loads) and read back with wave-uniform addresses (LDS broadcast).
-// Waves split the hidden units: wave w computes units [32w, 32w+32) of the concatenated
-// actor|critic layers (waves 0-1 actor, 2-3 critic), activations exchanged through LDS tiles
-// H1/H2 [128 units][64 envs].
-constexpr int PT_ENVS = 64, PT_THREADS = 256;
+// Policy tile: 64 envs (lane = env) x PT_WAVES waves. The whole parameter vector is staged in
+// LDS once per workgroup (wide coalesced loads) and read back with wave-uniform addresses (LDS
+// broadcast). Waves split the hidden units: wave w computes PT_UPW units of the concatenated
+// actor|critic layers (the first half of the waves the actor, the second the critic),
+// activations exchanged through LDS tiles H1/H2 [128 units][64 envs]. 4096 envs make only 64
+// workgroups, so the latency of a wave's unit loop is the kernel time: 16 waves (4 per SIMD)
+// hide the LDS reads and split the chain 4x finer than one wave per SIMD did (42 us -> see DESIGN).
+#ifndef PT_WAVES
+#define PT_WAVES 16
+#endif
+constexpr int PT_ENVS = 64, PT_THREADS = 64 * PT_WAVES, PT_HALF = PT_WAVES / 2, PT_UPW = H / PT_HALF;
+static_assert(H % PT_HALF == 0 && PT_WAVES >= 4, "policy tile split");
 struct PolicyLds {
   float w[P];
   float h1[2 * H * PT_ENVS];
@@ -179,15 +185,15 @@ __device__ __forceinline__ void stage_params(const float* __restrict__ p, float*
 // trunks of both nets for the tile; leaves H2 in LDS (caller syncs after)
 __device__ __forceinline__ void policy_trunks(PolicyLds& L, const float (&x)[NOBS], int lane, int wave,
                                               bool actor, bool critic) {
-  const bool mine = (wave < 2) ? actor : critic;
-  const Net net = (wave < 2) ? ACTOR : CRITIC;
-  const int u0 = (wave & 1) * 32;   // first unit of this wave within its net
-  const int hrow = (wave >> 1) * H;  // actor rows 0..63, critic rows 64..127
+  const bool mine = (wave < PT_HALF) ? actor : critic;
+  const Net net = (wave < PT_HALF) ? ACTOR : CRITIC;
+  const int u0 = (wave % PT_HALF) * PT_UPW;   // first unit of this wave within its net
+  const int hrow = (wave / PT_HALF) * H;        // actor rows 0..63, critic rows 64..127
   if (mine) {
     const float* W1 = L.w + net.w1;
     const float* b1 = L.w + net.b1;
 _Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + 32; u++) {
+    for (int u = u0; u < u0 + PT_UPW; u++) {
       float acc = 0.0f;
 #pragma unroll
       for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
@@ -202,7 +208,7 @@ _Pragma(PP_UNROLL_STR)
     const float* W2 = L.w + net.w2;
     const float* b2 = L.w + net.b2;
 _Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + 32; u++) {
+    for (int u = u0; u < u0 + PT_UPW; u++) {
       float acc = 0.0f;
 #pragma unroll
       for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
@@ -241,15 +247,15 @@ extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_act_kernel(ActAr
   float x[NOBS];
   load_obs_soa(A.obs, A.n, ec, x);
   __syncthreads();
-  if (A.obs_rows && valid && wave >= 2) {  // waves 2/3 copy the observation row (half each)
-    const int k0 = wave == 2 ? 0 : 40, k1 = wave == 2 ? 40 : NOBS;
+  if (A.obs_rows && valid && wave >= PT_WAVES - 2) {  // the last two waves copy the observation row
+    const int k0 = wave == PT_WAVES - 2 ? 0 : 40, k1 = wave == PT_WAVES - 2 ? 40 : NOBS;
 #pragma unroll
     for (int k = 0; k < NOBS; k++)
       if (k >= k0 && k < k1) A.obs_rows[(size_t)e * NOBS + k] = x[k];
   }
   policy_trunks(L, x, lane, wave, true, A.value != nullptr);
   if (!valid) return;
-  if (wave == 2 && A.value) A.value[e] = tile_value(L, lane);
+  if (wave == PT_HALF && A.value) A.value[e] = tile_value(L, lane);
   if (wave != 0) return;
   const float* p = L.w;
   float mu[NA], a[NA];
@@ -289,7 +295,7 @@ extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_value_kernel(con
   load_obs_soa(obs, n, ec, x);
   __syncthreads();
   policy_trunks(L, x, lane, wave, false, true);
-  if (e < n && wave == 2) value[e] = tile_value(L, lane);
+  if (e < n && wave == PT_HALF) value[e] = tile_value(L, lane);
 }
 
 // bootstrap: only tiles holding a truncated (not terminated) env run the critic
@@ -315,7 +321,7 @@ extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_bootstrap_kernel
     __syncthreads();
     policy_trunks(L, x, lane, wave, false, true);
   }
-  if (valid && wave == 2) {
+  if (valid && wave == PT_HALF) {
     float r = reward[e];
     if (boot) r += gamma * tile_value(L, lane);
     reward_out[e] = r;
@@ -827,10 +833,21 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
     if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
     grad[pidx] = s;
   }
-  if (blockIdx.x == 0 && threadIdx.x < ACKPPO_NLOSS) {
+  if (blockIdx.x == 0) {
+    // loss rows: 32 block-strided groups x 8 slots in parallel (a serial loop over the rows was
+    // a chain of dependent L2 round trips: 28 us at 256 rows), then an LDS tree over the groups
+    static_assert(ACKPPO_NLOSS == 8, "loss row layout");
+    __shared__ float lred[256];
+    const int slot = threadIdx.x & 7, grp = threadIdx.x >> 3;
     float s = 0.0f;
-    for (int b = 0; b < nblk; b++) s += lpart[(size_t)b * ACKPPO_NLOSS + threadIdx.x];
-    loss[threadIdx.x] = s;
+    for (int b = grp; b < nblk; b += 32) s += lpart[(size_t)b * ACKPPO_NLOSS + slot];
+    lred[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o >= 8; o >>= 1) {
+      if (threadIdx.x < o) lred[threadIdx.x] += lred[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x < ACKPPO_NLOSS) loss[threadIdx.x] = lred[threadIdx.x];
   }
 }
 
