@@ -115,6 +115,21 @@ int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg
                 float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
                 float* grad_norm_out, void* stream);
 
+/* One epoch of minibatch updates on a single rank (world 1: no all-reduce between the gradient
+ * and the Adam step). For m in [0, ceil(n_idx / batch)): ackppo_grad on idx[m * batch ...] with
+ * stats[2m .. 2m+1]; ackppo_reduce with the loss columns ADDED to loss_acc [8]; ackppo_adam with
+ * grad_scale 1 and t = adam_step0 + m + 1 (step_size = learning_rate / (1 - beta1^t), bc2_sqrt =
+ * sqrt(1 - beta2^t), float64 as torch computes them). The same kernels and arithmetic as the
+ * per-minibatch calls (SB3 PPO.train, on_policy_algorithm / ppo.py:196-279 of SB3 2.7.0); the
+ * loop runs on the host in C so the launches queue back to back. Data-parallel learners
+ * (world > 1) call grad / reduce / all-reduce / adam per minibatch instead. */
+int ackppo_epoch(float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
+                 const float* advantages, const float* returns, const int32_t* idx, int n_idx, int batch,
+                 const float* stats, float clip_range, float ent_coef, float vf_coef, float max_grad_norm,
+                 double learning_rate, double beta1, double beta2, float eps, int64_t adam_step0,
+                 float* grad_partial, float* loss_partial, float* grad, float* loss_acc, float* exp_avg,
+                 float* exp_avg_sq, float* grad_norm_out, void* stream);
+
 const char* ackppo_last_error(void);
 
 #ifdef __cplusplus

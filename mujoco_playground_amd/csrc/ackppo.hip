@@ -411,7 +411,10 @@ struct GradArgs {
 // row-major. Tile: GT samples, rows of GLDP floats (16-B aligned): X [80 rows], per net
 // h1, h2, d2, d1 [64 rows each], then gmu [2], glog [2], gv [1] rows.
 constexpr int GT = 32, GLDP = 36;
-constexpr int W_W1T = 0, W_W2_A = 160 * H, W_W2_C = W_W2_A + H * H;  // W1T: [80][128] = [k][actor|critic unit]
+// W1T: [80][W1T_LD] = [k][actor|critic unit] (row padded to 132 words: 16-B aligned rows whose
+// transposed staging writes spread over the LDS banks)
+constexpr int W1T_LD = 2 * H + 4;
+constexpr int W_W1T = 0, W_W2_A = 80 * W1T_LD, W_W2_C = W_W2_A + H * H;
 constexpr int W_B1_A = W_W2_C + H * H, W_B2_A = W_B1_A + H, W_B1_C = W_B2_A + H, W_B2_C = W_B1_C + H;
 constexpr int W_AW = W_B2_C + H, W_AB = W_AW + 2 * H, W_CW = W_AB + 4, W_CB = W_CW + H, W_LS = W_CB + 4;
 constexpr int W_TOTAL = W_LS + 4;
@@ -425,16 +428,36 @@ constexpr int GRAD_THREADS = 256;
 constexpr int GRAD_MAX_BLOCKS = 256;  // one workgroup per CU (the LDS footprint allows one)
 
 __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, float* w) {
-  // transposed first layers, both nets side by side (k row 79 = 0); consecutive threads write
-  // consecutive LDS words
-  for (int i = threadIdx.x; i < 80 * 2 * H; i += GRAD_THREADS) {
-    const int k = i / (2 * H), c = i - k * 2 * H, net = c >> 6, u = c & 63;
-    const int src = (net == 0 ? ACKPPO_OFF_PI_W1 : ACKPPO_OFF_VF_W1) + u * NOBS + k;
-    w[W_W1T + i] = k < NOBS ? p[src] : 0.0f;
+  // transposed first layers, both nets side by side (k row 79 = 0): coalesced global reads of
+  // the row-major [unit][79] weights, several loads in flight per thread (a strided read loop
+  // with one load outstanding cost 24k cycles per workgroup), transposed LDS writes
+  static_assert(ACKPPO_OFF_PI_W1 % 4 == 0 && ACKPPO_OFF_VF_W1 % 4 == 0 && (H * NOBS) % 4 == 0, "16-B W1 staging");
+  constexpr int N1 = H * NOBS / 4, IT1 = (2 * N1 + GRAD_THREADS - 1) / GRAD_THREADS;  // float4 per net, 10 per thread
+  float4 v[IT1];
+#pragma unroll
+  for (int j = 0; j < IT1; j++) {  // all loads in flight first (16 B per lane)
+    const int i = threadIdx.x + j * GRAD_THREADS, net = i >= N1;
+    if (i < 2 * N1) v[j] = reinterpret_cast<const float4*>(p + (net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1))[i - net * N1];
   }
-  for (int i = threadIdx.x; i < H * H; i += GRAD_THREADS) {
-    w[W_W2_A + i] = p[ACKPPO_OFF_PI_W2 + i];
-    w[W_W2_C + i] = p[ACKPPO_OFF_VF_W2 + i];
+#pragma unroll
+  for (int j = 0; j < IT1; j++) {
+    const int i = threadIdx.x + j * GRAD_THREADS, net = i >= N1;
+    if (i < 2 * N1) {
+      const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int r = 4 * (i - net * N1) + c, u = r / NOBS, k = r - u * NOBS;
+        w[W_W1T + k * W1T_LD + net * H + u] = e[c];
+      }
+    }
+  }
+  if (threadIdx.x < 2 * H) w[W_W1T + NOBS * W1T_LD + threadIdx.x] = 0.0f;
+  static_assert(ACKPPO_OFF_PI_W2 % 4 == 0 && ACKPPO_OFF_VF_W2 % 4 == 0 && W_W2_A % 4 == 0, "16-B W2 staging");
+#pragma unroll
+  for (int j = 0; j < H * H / 4 / GRAD_THREADS; j++) {
+    const int i = threadIdx.x + j * GRAD_THREADS;
+    reinterpret_cast<float4*>(w + W_W2_A)[i] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_PI_W2)[i];
+    reinterpret_cast<float4*>(w + W_W2_C)[i] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_VF_W2)[i];
   }
   for (int i = threadIdx.x; i < H; i += GRAD_THREADS) {
     w[W_B1_A + i] = p[ACKPPO_OFF_PI_B1 + i];
@@ -588,7 +611,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
       for (int i = 0; i < 16; i++) acc[i] = 0.0f;
 #pragma unroll 4
       for (int k = 0; k < 80; k++) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + W_W1T + k * 2 * H + 4 * ub);
+        const float4 wv = *reinterpret_cast<const float4*>(w + W_W1T + k * W1T_LD + 4 * ub);
         const float4 xv = *reinterpret_cast<const float4*>(tl + G_X + k * GLDP + gs);
         const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
@@ -824,7 +847,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(cons
 }
 extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const float* tmp, int rg, const float* lpart,
                                                                        int nblk, float ent_coef, float* grad,
-                                                                       float* loss) {
+                                                                       float* loss, int accumulate) {
   const int pidx = blockIdx.x * 256 + threadIdx.x;
   if (pidx < P) {
     float s = 0.0f;
@@ -847,7 +870,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
       if (threadIdx.x < o) lred[threadIdx.x] += lred[threadIdx.x + o];
       __syncthreads();
     }
-    if (threadIdx.x < ACKPPO_NLOSS) loss[threadIdx.x] = lred[threadIdx.x];
+    if (threadIdx.x < ACKPPO_NLOSS) loss[threadIdx.x] = (accumulate ? loss[threadIdx.x] : 0.0f) + lred[threadIdx.x];
   }
 }
 
@@ -1005,17 +1028,24 @@ int ackppo_grad_blocks(int batch) {
   return tiles < GRAD_MAX_BLOCKS ? tiles : GRAD_MAX_BLOCKS;
 }
 
-int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
-                  float* loss, void* stream) {
-  if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0) return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments");
+namespace {
+int reduce_launch(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+                  float* loss, int accumulate, void* stream) {
   const int rg = nblk < REDUCE_RG ? nblk : REDUCE_RG;
   if (!g_reduce_tmp && hipMalloc(&g_reduce_tmp, sizeof(float) * P * REDUCE_RG) != hipSuccess)
     return fail(ACKPPO_EHIP, "ackppo_reduce: scratch allocation");
   hipLaunchKernelGGL(ackppo_reduce_rows_kernel, dim3((P + 255) / 256, rg), dim3(256), 0, (hipStream_t)stream,
                      grad_partial, nblk, g_reduce_tmp);
   hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, g_reduce_tmp, rg,
-                     loss_partial, nblk, ent_coef, grad, loss);
+                     loss_partial, nblk, ent_coef, grad, loss, accumulate);
   return launched("ackppo_reduce");
+}
+}  // namespace
+
+int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+                  float* loss, void* stream) {
+  if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0) return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments");
+  return reduce_launch(grad_partial, loss_partial, nblk, ent_coef, grad, loss, 0, stream);
 }
 
 int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
@@ -1026,6 +1056,33 @@ int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg
                      exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
                      grad_norm_out);
   return launched("ackppo_adam");
+}
+
+int ackppo_epoch(float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
+                 const float* advantages, const float* returns, const int32_t* idx, int n_idx, int batch,
+                 const float* stats, float clip_range, float ent_coef, float vf_coef, float max_grad_norm,
+                 double learning_rate, double beta1, double beta2, float eps, int64_t adam_step0,
+                 float* grad_partial, float* loss_partial, float* grad, float* loss_acc, float* exp_avg,
+                 float* exp_avg_sq, float* grad_norm_out, void* stream) {
+  if (!params || !obs_rows || !actions || !old_log_prob || !advantages || !returns || !idx || !stats ||
+      !grad_partial || !loss_partial || !grad || !loss_acc || !exp_avg || !exp_avg_sq || n_idx < 0 || batch <= 0 ||
+      adam_step0 < 0)
+    return fail(ACKPPO_EINVAL, "ackppo_epoch: bad arguments");
+  const int nmb = (n_idx + batch - 1) / batch;
+  for (int m = 0; m < nmb; m++) {
+    const int nb = n_idx - m * batch < batch ? n_idx - m * batch : batch;
+    int rc = ackppo_grad(params, obs_rows, actions, old_log_prob, advantages, returns, idx + (size_t)m * batch, nb,
+                         stats + 2 * m, clip_range, ent_coef, vf_coef, grad_partial, loss_partial, stream);
+    if (rc) return rc;
+    rc = reduce_launch(grad_partial, loss_partial, ackppo_grad_blocks(nb), ent_coef, grad, loss_acc, 1, stream);
+    if (rc) return rc;
+    const double t = (double)(adam_step0 + m + 1);  // torch's bias corrections, in float64 as the host path
+    rc = ackppo_adam(params, grad, exp_avg, exp_avg_sq, 1.0f, max_grad_norm, (float)beta1, (float)beta2, eps,
+                     (float)(learning_rate / (1.0 - pow(beta1, t))), (float)sqrt(1.0 - pow(beta2, t)), grad_norm_out,
+                     stream);
+    if (rc) return rc;
+  }
+  return ACKPPO_OK;
 }
 
 }  // extern "C"

@@ -149,6 +149,7 @@ class PPO:
         self.grad = torch.zeros(NPARAM, **f32)
         self.loss = torch.zeros(NLOSS, **f32)
         self.loss_acc = torch.zeros(NLOSS, **f32)
+        self.fused_epoch = True  # world 1: ackppo_epoch (same kernels and scalars as the per-minibatch calls)
         self.gnorm = torch.zeros(1, **f32)
         nmb = (T * N + batch_size - 1) // batch_size
         self.mb_stats = torch.zeros(nmb, 2, **f32)
@@ -233,6 +234,16 @@ class PPO:
             perm = torch.randperm(S, device=self.device, generator=self.perm_gen).to(torch.int32)
             _lib.ppo_check(L.ackppo_adv_stats(_ptr(self.buf_adv), _ptr(perm), S, B, int(self.normalize_advantage),
                                               _ptr(self.mb_stats), s), "ackppo_adv_stats")
+            if self.world == 1 and self.fused_epoch:  # one C call per epoch: grad -> reduce -> adam per minibatch
+                _lib.ppo_check(L.ackppo_epoch(_ptr(self.params), _ptr(self.buf_obs), _ptr(self.buf_act),
+                                              _ptr(self.buf_logp), _ptr(self.buf_adv), _ptr(self.buf_ret), _ptr(perm),
+                                              S, B, _ptr(self.mb_stats), self.clip_range, self.ent_coef, self.vf_coef,
+                                              self.max_grad_norm, self.learning_rate, b1, b2, 1e-5, self.adam_step,
+                                              _ptr(self.gpart), _ptr(self.lpart), _ptr(self.grad),
+                                              _ptr(self.loss_acc), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
+                                              _ptr(self.gnorm), s), "ackppo_epoch")
+                self.adam_step += nmb
+                continue
             for m in range(nmb):
                 nb = min(B, S - m * B)
                 idx = perm[m * B:]

@@ -171,6 +171,24 @@ def test_ppo_learn_end_to_end():
     assert a.shape == (256, 2) and float(a.abs().max()) <= 1.0
 
 
+def test_fused_epoch_matches_per_minibatch_calls():
+    """ackppo_epoch (one C call per epoch) and the per-minibatch grad/reduce/adam calls give
+    bit-identical parameters, Adam moments and loss statistics."""
+    from mujoco_playground_amd.rl import make_ackermann_env
+    from mujoco_playground_amd.rl.ppo import PPO
+    out = []
+    for fused in (True, False):
+        venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01)
+        model.fused_epoch = fused
+        model.learn(total_timesteps=2 * 16 * 256)
+        out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
+                    model.logger["train/value_loss"], model.logger["train/approx_kl"]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert out[0][2:] == out[1][2:]
+
+
 def _ppo_rank(rank, world, port, q):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),

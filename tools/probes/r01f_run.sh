@@ -1,7 +1,6 @@
+#!/bin/bash
+# r01f GPU probe: PPO GPU tests, bench (no CPU leg).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest.log 2>&1
-rc=$?
-[ $rc -le 1 ] || exit $rc
-bash tools/variant_sweep.sh qbase qsmooth > gpurun_out/sweep.log 2>&1 || exit 1
-exit $rc
+timeout -k 10 200 python -u -m pytest tests/test_gpu_ppo.py -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_ppo.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --no-cpu > gpurun_out/bench.json 2> gpurun_out/bench.err
