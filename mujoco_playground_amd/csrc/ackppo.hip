@@ -411,10 +411,12 @@ struct GradArgs {
 // row-major. Tile: GT samples, rows of GLDP floats (16-B aligned): X [80 rows], per net
 // h1, h2, d2, d1 [64 rows each], then gmu [2], glog [2], gv [1] rows.
 constexpr int GT = 32, GLDP = 36;
-// W1T: [80][W1T_LD] = [k][actor|critic unit] (row padded to 132 words: 16-B aligned rows whose
-// transposed staging writes spread over the LDS banks)
-constexpr int W1T_LD = 2 * H + 4;
-constexpr int W_W1T = 0, W_W2_A = 80 * W1T_LD, W_W2_C = W_W2_A + H * H;
+// W1T: [80][128] = [k][actor|critic unit], W2: [unit][k] row-major per net. Both are XOR-swizzled
+// (w1t_at / w2_at) so the MFMA operand reads -- 16 consecutive units x 4 consecutive k per wave --
+// hit 64 distinct LDS banks (W1T, layer-2 W2 reads) or at most 4 lanes per bank (W2^T reads).
+constexpr int W_W1T = 0, W_W2_A = 80 * 2 * H, W_W2_C = W_W2_A + H * H;
+__device__ __forceinline__ int w1t_at(int k, int c) { return W_W1T + k * 2 * H + (c ^ (16 * (k & 3))); }
+__device__ __forceinline__ int w2_at(int u, int k) { return u * H + (k ^ (4 * (u & 15))); }
 constexpr int W_B1_A = W_W2_C + H * H, W_B2_A = W_B1_A + H, W_B1_C = W_B2_A + H, W_B2_C = W_B1_C + H;
 constexpr int W_AW = W_B2_C + H, W_AB = W_AW + 2 * H, W_CW = W_AB + 4, W_CB = W_CW + H, W_LS = W_CB + 4;
 constexpr int W_TOTAL = W_LS + 4;
@@ -447,17 +449,31 @@ __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, 
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const int r = 4 * (i - net * N1) + c, u = r / NOBS, k = r - u * NOBS;
-        w[W_W1T + k * W1T_LD + net * H + u] = e[c];
+        w[w1t_at(k, net * H + u)] = e[c];
       }
     }
   }
-  if (threadIdx.x < 2 * H) w[W_W1T + NOBS * W1T_LD + threadIdx.x] = 0.0f;
-  static_assert(ACKPPO_OFF_PI_W2 % 4 == 0 && ACKPPO_OFF_VF_W2 % 4 == 0 && W_W2_A % 4 == 0, "16-B W2 staging");
+  if (threadIdx.x < 2 * H) w[w1t_at(NOBS, threadIdx.x)] = 0.0f;
+  static_assert(ACKPPO_OFF_PI_W2 % 4 == 0 && ACKPPO_OFF_VF_W2 % 4 == 0, "16-B W2 loads");
+  {
+    constexpr int IT2 = H * H / 4 / GRAD_THREADS;
+    float4 va[IT2], vc[IT2];
 #pragma unroll
-  for (int j = 0; j < H * H / 4 / GRAD_THREADS; j++) {
-    const int i = threadIdx.x + j * GRAD_THREADS;
-    reinterpret_cast<float4*>(w + W_W2_A)[i] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_PI_W2)[i];
-    reinterpret_cast<float4*>(w + W_W2_C)[i] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_VF_W2)[i];
+    for (int j = 0; j < IT2; j++) {
+      const int i = threadIdx.x + j * GRAD_THREADS;
+      va[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_PI_W2)[i];
+      vc[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_VF_W2)[i];
+    }
+#pragma unroll
+    for (int j = 0; j < IT2; j++) {
+      const int i = 4 * (threadIdx.x + j * GRAD_THREADS), u = i / H, k = i - u * H;  // 4 k of one row
+      const float ea[4] = {va[j].x, va[j].y, va[j].z, va[j].w}, ec[4] = {vc[j].x, vc[j].y, vc[j].z, vc[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        w[W_W2_A + w2_at(u, k + c)] = ea[c];
+        w[W_W2_C + w2_at(u, k + c)] = ec[c];
+      }
+    }
   }
   for (int i = threadIdx.x; i < H; i += GRAD_THREADS) {
     w[W_B1_A + i] = p[ACKPPO_OFF_PI_B1 + i];
@@ -475,29 +491,6 @@ __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, 
   if (threadIdx.x == 0) w[W_CB] = p[ACKPPO_OFF_VAL_B];
 }
 
-// sum over the GT samples of a[r][s] * b[c][s] for a 4x4 block of rows, added into acc
-__device__ __forceinline__ void outer4x4_acc(const float* a, const float* b, float acc[16]) {
-#pragma unroll 2
-  for (int s = 0; s < GT; s += 4) {
-    float4 av[4], bv[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      av[i] = *reinterpret_cast<const float4*>(a + i * GLDP + s);
-      bv[i] = *reinterpret_cast<const float4*>(b + i * GLDP + s);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        float t = acc[4 * i + j];
-        t = fmaf(av[i].x, bv[j].x, t);
-        t = fmaf(av[i].y, bv[j].y, t);
-        t = fmaf(av[i].z, bv[j].z, t);
-        t = fmaf(av[i].w, bv[j].w, t);
-        acc[4 * i + j] = t;
-      }
-  }
-}
 __device__ __forceinline__ float row_sum_g(const float* a) {
   float s = 0.0f;
 #pragma unroll
@@ -520,11 +513,16 @@ __device__ __forceinline__ float row_dot_g(const float* a, const float* b) {
   return s;
 }
 
-// weight-gradient work items of one thread: first-layer 4x4 blocks (2 nets x 16 x 20 = 640),
-// second-layer 4x4 blocks (2 x 16 x 16 = 512), vector entries (453; see vec_item)
-constexpr int NB1 = 640, NB2 = 512, NVEC = 453;
-constexpr int PER1 = (NB1 + GRAD_THREADS - 1) / GRAD_THREADS, PER2 = NB2 / GRAD_THREADS;
+// vector gradient entries (biases, heads, log_std: 453; see vec_item), PERV per thread
+constexpr int NVEC = 453;
 constexpr int PERV = (NVEC + GRAD_THREADS - 1) / GRAD_THREADS;
+
+// f32 MFMA 16x16x4 (exact f32 products, k-ordered fmaf chain): lane l supplies A[l & 15][l >> 4]
+// and B[l >> 4][l & 15]; D[row 4 (l >> 4) + r][col l & 15] comes back in element r.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 __device__ __forceinline__ float vec_item(const float* tl, int i) {
   const float* an = tl + G_NET;
@@ -568,15 +566,21 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   const float invB = 1.0f / (float)A.batch;
   stage_grad_weights(A.params, w);
 
-  float acc1[PER1][16], acc2[PER2][16], accv[PERV];
+  // MFMA tiles: lane (li, lk) = (lane & 15, lane >> 4). Wave w owns unit tiles ut = 2w, 2w + 1
+  // of the 128 actor|critic units (16 each; its net is w >> 1, its units within the net
+  // 32 (w & 1) + 16 t + ...) in every GEMM below. Weight gradients stay in the accumulators
+  // across tiles: gW1 [2 unit tiles][5 k tiles of the 80 inputs], gW2 [2][4 k tiles of 64].
+  const int li = lane & 15, lk = lane >> 4;
+  const int ub0 = 32 * (wave & 1);  // first unit (within the wave's net) of the wave's two tiles
+  f4v gw1[2][5], gw2[2][4];
 #pragma unroll
-  for (int b = 0; b < PER1; b++)
+  for (int t = 0; t < 2; t++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) acc1[b][i] = 0.0f;
+    for (int j = 0; j < 5; j++) gw1[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int b = 0; b < PER2; b++)
-#pragma unroll
-    for (int i = 0; i < 16; i++) acc2[b][i] = 0.0f;
+    for (int j = 0; j < 4; j++) gw2[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  float accv[PERV];
 #pragma unroll
   for (int b = 0; b < PERV; b++) accv[b] = 0.0f;
   float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
@@ -605,51 +609,62 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     // GEMM-shaped layers: thread (ub, sb) owns 4 units (of the 128 actor|critic units) x 4 samples
     const int ub = tid >> 3, sb = tid & 7, gnet = ub >> 4, gu = 4 * (ub & 15), gs = 4 * sb;
     float* gt = tl + G_NET + gnet * G_NETSZ;  // this thread's net tile
-    {  // layer 1: H1 = tanh(W1 X + b1), k-outer, two 16-B LDS reads per 16 FMAs
-      float acc[16];
+    {  // layer 1: H1 = tanh(W1 X + b1): [128 units x 32 samples] = W1T^T [128 x 80] . X [80 x 32]
+      f4v acc[2][2];
 #pragma unroll
-      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 4
-      for (int k = 0; k < 80; k++) {
-        const float4 wv = *reinterpret_cast<const float4*>(w + W_W1T + k * W1T_LD + 4 * ub);
-        const float4 xv = *reinterpret_cast<const float4*>(tl + G_X + k * GLDP + gs);
-        const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, xa[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int j = 0; j < 4; j++) acc[4 * i + j] = fmaf(wa[i], xa[j], acc[4 * i + j]);
+      for (int k0 = 0; k0 < 80; k0 += 4) {
+        const int k = k0 + lk;
+        const float a0 = w[w1t_at(k, nid * H + ub0 + li)], a1 = w[w1t_at(k, nid * H + ub0 + 16 + li)];
+        const float b0 = tl[G_X + k * GLDP + li], b1 = tl[G_X + k * GLDP + 16 + li];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
-      const float* b1 = w + (gnet == 0 ? W_B1_A : W_B1_C);
+      const float* bias = w + (nid ? W_B1_C : W_B1_A);
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const float4 o = make_float4(tanhf(acc[4 * i] + b1[gu + i]), tanhf(acc[4 * i + 1] + b1[gu + i]),
-                                     tanhf(acc[4 * i + 2] + b1[gu + i]), tanhf(acc[4 * i + 3] + b1[gu + i]));
-        *reinterpret_cast<float4*>(gt + G_H1 + (gu + i) * GLDP + gs) = o;
-      }
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = ub0 + 16 * t + 4 * lk + r;
+          const float bb = bias[u];
+#pragma unroll
+          for (int j = 0; j < 2; j++) nt[G_H1 + u * GLDP + 16 * j + li] = tanhf(acc[t][j][r] + bb);
+        }
     }
     __syncthreads();
     PSTAMP(2);
-    {  // layer 2: H2 = tanh(W2 H1 + b2) per net (row-major W2: four 4-B reads + one 16-B read per 16 FMAs)
-      float acc[16];
+    {  // layer 2: H2 = tanh(W2 H1 + b2) per net: [64 x 32] = W2 [64 x 64] . H1 [64 x 32]
+      const float* W2 = w + (nid ? W_W2_C : W_W2_A);
+      f4v acc[2][2];
 #pragma unroll
-      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
-      const float* W2 = w + (gnet == 0 ? W_W2_A : W_W2_C) + gu * H;
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 4
-      for (int k = 0; k < H; k++) {
-        const float4 hv = *reinterpret_cast<const float4*>(gt + G_H1 + k * GLDP + gs);
-        const float wa[4] = {W2[k], W2[H + k], W2[2 * H + k], W2[3 * H + k]}, ha[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int j = 0; j < 4; j++) acc[4 * i + j] = fmaf(wa[i], ha[j], acc[4 * i + j]);
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;
+        const float a0 = W2[w2_at(ub0 + li, k)], a1 = W2[w2_at(ub0 + 16 + li, k)];
+        const float b0 = nt[G_H1 + k * GLDP + li], b1 = nt[G_H1 + k * GLDP + 16 + li];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
-      const float* b2 = w + (gnet == 0 ? W_B2_A : W_B2_C);
+      const float* bias = w + (nid ? W_B2_C : W_B2_A);
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const float4 o = make_float4(tanhf(acc[4 * i] + b2[gu + i]), tanhf(acc[4 * i + 1] + b2[gu + i]),
-                                     tanhf(acc[4 * i + 2] + b2[gu + i]), tanhf(acc[4 * i + 3] + b2[gu + i]));
-        *reinterpret_cast<float4*>(gt + G_H2 + (gu + i) * GLDP + gs) = o;
-      }
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = ub0 + 16 * t + 4 * lk + r;
+          const float bb = bias[u];
+#pragma unroll
+          for (int j = 0; j < 2; j++) nt[G_H2 + u * GLDP + 16 * j + li] = tanhf(acc[t][j][r] + bb);
+        }
     }
     __syncthreads();
     PSTAMP(3);
@@ -730,46 +745,56 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     }
     __syncthreads();
     PSTAMP(5);
-    {  // d1 = (W2^T d2) (1 - h1^2): j-outer over row-major W2, two 16-B reads per 16 FMAs
-      float acc[16];
+    {  // d1 = (W2^T d2) (1 - h1^2): [64 x 32] = W2^T [64 x 64] . D2 [64 x 32] per net
+      const float* W2 = w + (nid ? W_W2_C : W_W2_A);
+      f4v acc[2][2];
 #pragma unroll
-      for (int i = 0; i < 16; i++) acc[i] = 0.0f;
-      const float* W2 = w + (gnet == 0 ? W_W2_A : W_W2_C) + gu;
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 4
-      for (int j = 0; j < H; j++) {
-        const float4 wv = *reinterpret_cast<const float4*>(W2 + j * H);
-        const float4 dv = *reinterpret_cast<const float4*>(gt + G_D2 + j * GLDP + gs);
-        const float wa[4] = {wv.x, wv.y, wv.z, wv.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int jj = 0; jj < 4; jj++) acc[4 * i + jj] = fmaf(wa[i], da[jj], acc[4 * i + jj]);
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;  // layer-2 unit
+        const float a0 = W2[w2_at(k, ub0 + li)], a1 = W2[w2_at(k, ub0 + 16 + li)];
+        const float b0 = nt[G_D2 + k * GLDP + li], b1 = nt[G_D2 + k * GLDP + 16 + li];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const float4 h1 = *reinterpret_cast<const float4*>(gt + G_H1 + (gu + i) * GLDP + gs);
-        const float4 o = make_float4(acc[4 * i] * (1.0f - h1.x * h1.x), acc[4 * i + 1] * (1.0f - h1.y * h1.y),
-                                     acc[4 * i + 2] * (1.0f - h1.z * h1.z), acc[4 * i + 3] * (1.0f - h1.w * h1.w));
-        *reinterpret_cast<float4*>(gt + G_D1 + (gu + i) * GLDP + gs) = o;
-      }
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = ub0 + 16 * t + 4 * lk + r;
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            const float h1 = nt[G_H1 + u * GLDP + 16 * j + li];
+            nt[G_D1 + u * GLDP + 16 * j + li] = acc[t][j][r] * (1.0f - h1 * h1);
+          }
+        }
     }
     __syncthreads();
     PSTAMP(6);
-    // weight-gradient sums over the tile (rows of padding samples are zero)
+    // weight-gradient sums over the tile's samples (rows of padding samples are zero):
+    // gW1 [units x 80] += D1 [units x 32] . X^T [32 x 80], gW2 [units x 64] += D2 . H1^T
+#pragma unroll 2
+    for (int q0 = 0; q0 < GT; q0 += 4) {
+      const int q = q0 + lk;  // sample
+      const float a0 = nt[G_D1 + (ub0 + li) * GLDP + q], a1 = nt[G_D1 + (ub0 + 16 + li) * GLDP + q];
+      const float c0 = nt[G_D2 + (ub0 + li) * GLDP + q], c1 = nt[G_D2 + (ub0 + 16 + li) * GLDP + q];
 #pragma unroll
-    for (int bb = 0; bb < PER1; bb++) {
-      const int b = tid + bb * GRAD_THREADS;
-      if (b < NB1) {
-        const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
-        outer4x4_acc(tl + G_NET + nn * G_NETSZ + G_D1 + 4 * jb * GLDP, tl + G_X + 4 * kb * GLDP, acc1[bb]);
+      for (int j = 0; j < 5; j++) {
+        const float bx = tl[G_X + (16 * j + li) * GLDP + q];
+        gw1[0][j] = mfma4(a0, bx, gw1[0][j]);
+        gw1[1][j] = mfma4(a1, bx, gw1[1][j]);
       }
-    }
 #pragma unroll
-    for (int bb = 0; bb < PER2; bb++) {
-      const int b = tid + bb * GRAD_THREADS;
-      const int nn = b / 256, r = b - nn * 256, jb = r / 16, kb = r - jb * 16;
-      const float* nb = tl + G_NET + nn * G_NETSZ;
-      outer4x4_acc(nb + G_D2 + 4 * jb * GLDP, nb + G_H1 + 4 * kb * GLDP, acc2[bb]);
+      for (int j = 0; j < 4; j++) {
+        const float bh = nt[G_H1 + (16 * j + li) * GLDP + q];
+        gw2[0][j] = mfma4(c0, bh, gw2[0][j]);
+        gw2[1][j] = mfma4(c1, bh, gw2[1][j]);
+      }
     }
 #pragma unroll
     for (int bb = 0; bb < PERV; bb++) {
@@ -780,28 +805,19 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   PSTAMP(7);
   // this workgroup's partial gradient row and loss sums
   float* g = A.gpart + (size_t)blockIdx.x * P;
+  {
+    const int w1 = nid ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, w2 = nid ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
 #pragma unroll
-  for (int bb = 0; bb < PER1; bb++) {
-    const int b = tid + bb * GRAD_THREADS;
-    if (b < NB1) {
-      const int nn = b / 320, r = b - nn * 320, jb = r / 20, kb = r - jb * 20;
-      const int w1 = nn == 0 ? ACKPPO_OFF_PI_W1 : ACKPPO_OFF_VF_W1;
+    for (int t = 0; t < 2; t++)
 #pragma unroll
-      for (int i = 0; i < 4; i++)
+      for (int r = 0; r < 4; r++) {
+        const int u = ub0 + 16 * t + 4 * lk + r;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (4 * kb + j < NOBS) g[w1 + (4 * jb + i) * NOBS + 4 * kb + j] = acc1[bb][4 * i + j];
-    }
-  }
+        for (int j = 0; j < 5; j++)
+          if (16 * j + li < NOBS) g[w1 + u * NOBS + 16 * j + li] = gw1[t][j][r];
 #pragma unroll
-  for (int bb = 0; bb < PER2; bb++) {
-    const int b = tid + bb * GRAD_THREADS;
-    const int nn = b / 256, r = b - nn * 256, jb = r / 16, kb = r - jb * 16;
-    const int w2 = nn == 0 ? ACKPPO_OFF_PI_W2 : ACKPPO_OFF_VF_W2;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) g[w2 + (4 * jb + i) * H + 4 * kb + j] = acc2[bb][4 * i + j];
+        for (int j = 0; j < 4; j++) g[w2 + u * H + 16 * j + li] = gw2[t][j][r];
+      }
   }
 #pragma unroll
   for (int bb = 0; bb < PERV; bb++) {
