@@ -235,53 +235,6 @@ __device__ __forceinline__ void tile_mu(const PolicyLds& L, int lane, float mu[N
   }
 }
 
-extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_act_kernel(ActArgs A) {
-  extern __shared__ float lds_raw[];
-  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int e = blockIdx.x * PT_ENVS + lane;
-  const bool valid = e < A.n;
-  const int ec = valid ? e : A.n - 1;  // padding lanes recompute the last env, write nothing
-  stage_params(A.params, L.w);
-  float x[NOBS];
-  load_obs_soa(A.obs, A.n, ec, x);
-  __syncthreads();
-  if (A.obs_rows && valid && wave >= PT_WAVES - 2) {  // the last two waves copy the observation row
-    const int k0 = wave == PT_WAVES - 2 ? 0 : 40, k1 = wave == PT_WAVES - 2 ? 40 : NOBS;
-#pragma unroll
-    for (int k = 0; k < NOBS; k++)
-      if (k >= k0 && k < k1) A.obs_rows[(size_t)e * NOBS + k] = x[k];
-  }
-  policy_trunks(L, x, lane, wave, true, A.value != nullptr);
-  if (!valid) return;
-  if (wave == PT_HALF && A.value) A.value[e] = tile_value(L, lane);
-  if (wave != 0) return;
-  const float* p = L.w;
-  float mu[NA], a[NA];
-  tile_mu(L, lane, mu);
-  if (A.deterministic) {
-    a[0] = mu[0];
-    a[1] = mu[1];
-  } else {
-    uint32_t c[4] = {(uint32_t)(A.env_offset + e), A.step, 2u, 0u};
-    philox(c, (uint32_t)A.seed, (uint32_t)(A.seed >> 32));
-    const float u1 = (float)((c[0] >> 8) + 1u) * (1.0f / 16777216.0f);  // (0, 1]
-    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);         // [0, 1)
-    const float r = sqrtf(-2.0f * logf(u1));
-    const float z[NA] = {r * cosf(TWO_PI * u2), r * sinf(TWO_PI * u2)};
-#pragma unroll
-    for (int d = 0; d < NA; d++) a[d] = mu[d] + expf(p[ACKPPO_OFF_LOG_STD + d]) * z[d];
-  }
-  if (A.action) {
-    A.action[2 * (size_t)e] = a[0];
-    A.action[2 * (size_t)e + 1] = a[1];
-  }
-  A.env_action[2 * (size_t)e] = fminf(fmaxf(a[0], -1.0f), 1.0f);
-  A.env_action[2 * (size_t)e + 1] = fminf(fmaxf(a[1], -1.0f), 1.0f);
-  if (A.log_prob) A.log_prob[e] = gauss_logp(a, mu, p);
-}
-
 extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_value_kernel(const float* params, const float* obs,
                                                                              int n, float* value) {
   extern __shared__ float lds_raw[];
@@ -845,6 +798,122 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   PSTAMP(15);
 }
 
+// ---- ackppo_act: MFMA policy tile. 16 envs per 256-lane workgroup (4096 envs = 256 workgroups,
+// one per CU): the weights are staged as in ackppo_grad (transposed / swizzled), X [80][16],
+// H1 / H2 [128 units][16 envs] in LDS; wave w computes unit tiles 2w, 2w + 1 of both layers as
+// 16x16 f32 MFMA tiles (k-ordered fmaf chains, like the grad kernel's forward pass); wave 0 then
+// evaluates the heads (lanes (env, output): mu0, mu1, value) and samples the actions.
+constexpr int AE = 16;  // envs per workgroup
+constexpr int A_X = W_TOTAL, A_H1 = A_X + 80 * AE, A_H2 = A_H1 + 2 * H * AE, A_TOTAL = A_H2 + 2 * H * AE;
+constexpr size_t ACT_LDS = (size_t)A_TOTAL * sizeof(float);
+
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(ActArgs A) {
+  extern __shared__ float tl[];
+  float* w = tl;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  const int e0 = blockIdx.x * AE, nv = min(AE, A.n - e0);
+  stage_grad_weights(A.params, w);
+  {  // X [k][env] from the SoA observation (row 79 and padding envs zero)
+    const int e = tid & 15;
+#pragma unroll
+    for (int k = tid >> 4; k < 80; k += 16)
+      tl[A_X + k * AE + e] = (k < NOBS && e < nv) ? A.obs[(size_t)k * A.n + e0 + e] : 0.0f;
+  }
+  __syncthreads();
+  if (A.obs_rows) {  // rollout-buffer rows [env][79]: one contiguous block of nv * 79 words
+    for (int i = tid; i < nv * NOBS; i += GRAD_THREADS) {
+      const int e = i / NOBS, k = i - e * NOBS;
+      A.obs_rows[(size_t)e0 * NOBS + i] = tl[A_X + k * AE + e];
+    }
+  }
+  const int nid = wave >> 1, ub0 = 32 * (wave & 1);
+  {  // layer 1: [128 x 16] = W1T^T [128 x 80] . X [80 x 16]
+    f4v acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 5
+    for (int k0 = 0; k0 < 80; k0 += 4) {
+      const int k = k0 + lk;
+      const float b = tl[A_X + k * AE + li];
+      acc0 = mfma4(w[w1t_at(k, nid * H + ub0 + li)], b, acc0);
+      acc1 = mfma4(w[w1t_at(k, nid * H + ub0 + 16 + li)], b, acc1);
+    }
+    const float* bias = w + (nid ? W_B1_C : W_B1_A);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int u = ub0 + 4 * lk + r;
+      tl[A_H1 + (nid * H + u) * AE + li] = tanhf(acc0[r] + bias[u]);
+      tl[A_H1 + (nid * H + u + 16) * AE + li] = tanhf(acc1[r] + bias[u + 16]);
+    }
+  }
+  __syncthreads();
+  {  // layer 2 per net: [64 x 16] = W2 [64 x 64] . H1 [64 x 16]
+    const float* W2 = w + (nid ? W_W2_C : W_W2_A);
+    const float* h1 = tl + A_H1 + nid * H * AE;
+    f4v acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
+    for (int k0 = 0; k0 < H; k0 += 4) {
+      const int k = k0 + lk;
+      const float b = h1[k * AE + li];
+      acc0 = mfma4(W2[w2_at(ub0 + li, k)], b, acc0);
+      acc1 = mfma4(W2[w2_at(ub0 + 16 + li, k)], b, acc1);
+    }
+    const float* bias = w + (nid ? W_B2_C : W_B2_A);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int u = ub0 + 4 * lk + r;
+      tl[A_H2 + (nid * H + u) * AE + li] = tanhf(acc0[r] + bias[u]);
+      tl[A_H2 + (nid * H + u + 16) * AE + li] = tanhf(acc1[r] + bias[u + 16]);
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // heads: lane (env li, output lk): 0 mu0, 1 mu1 (actor H2 rows 0-63), 2 value (critic rows 64-127)
+  float v = 0.0f;
+  {
+    const int wo = lk == 0 ? W_AW : (lk == 1 ? W_AW + H : W_CW);
+    const float* h2 = tl + A_H2 + (lk == 2 ? H * AE : 0);
+#pragma unroll 8
+    for (int j = 0; j < H; j++) v = fmaf(w[wo + j], h2[j * AE + li], v);
+    v += lk == 0 ? w[W_AB] : (lk == 1 ? w[W_AB + 1] : w[W_CB]);
+  }
+  const float mu1 = __shfl(v, li + 16, 64), val = __shfl(v, li + 32, 64);
+  if (lk != 0 || li >= nv) return;
+  const int e = e0 + li;
+  const float mu[NA] = {v, mu1};
+  float a[NA];
+  if (A.deterministic) {
+    a[0] = mu[0];
+    a[1] = mu[1];
+  } else {
+    uint32_t c[4] = {(uint32_t)(A.env_offset + e), A.step, 2u, 0u};
+    philox(c, (uint32_t)A.seed, (uint32_t)(A.seed >> 32));
+    const float u1 = (float)((c[0] >> 8) + 1u) * (1.0f / 16777216.0f);  // (0, 1]
+    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);         // [0, 1)
+    const float r = sqrtf(-2.0f * logf(u1));
+    const float z[NA] = {r * cosf(TWO_PI * u2), r * sinf(TWO_PI * u2)};
+#pragma unroll
+    for (int d = 0; d < NA; d++) a[d] = mu[d] + expf(w[W_LS + d]) * z[d];
+  }
+  if (A.action) {
+    A.action[2 * (size_t)e] = a[0];
+    A.action[2 * (size_t)e + 1] = a[1];
+  }
+  A.env_action[2 * (size_t)e] = fminf(fmaxf(a[0], -1.0f), 1.0f);
+  A.env_action[2 * (size_t)e + 1] = fminf(fmaxf(a[1], -1.0f), 1.0f);
+  if (A.log_prob) {
+    float lp = 0.0f;
+#pragma unroll
+    for (int d = 0; d < NA; d++) {  // gauss_logp with the staged log_std
+      const float sigma = expf(w[W_LS + d]);
+      const float dv = a[d] - mu[d];
+      lp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
+    }
+    A.log_prob[e] = lp;
+  }
+  if (A.value) A.value[e] = val;
+}
+
 // Two passes, no atomics: (1) grid (param blocks of 256, REDUCE_RG row groups) sums rows
 // by, by + RG, ... into tmp[by][p] with 4 loads in flight per thread; (2) sums the RG rows.
 constexpr int REDUCE_RG = 16;
@@ -944,11 +1013,13 @@ float* g_reduce_tmp = nullptr;  // [REDUCE_RG][NPARAM] row-group sums (one small
 bool g_policy_attr = false;
 bool policy_lds_ready() {
   if (g_policy_attr) return true;
-  const void* ks[3] = {(const void*)ackppo_act_kernel, (const void*)ackppo_value_kernel,
-                       (const void*)ackppo_bootstrap_kernel};
+  const void* ks[2] = {(const void*)ackppo_value_kernel, (const void*)ackppo_bootstrap_kernel};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(PolicyLds)) != hipSuccess)
       return false;
+  if (hipFuncSetAttribute((const void*)ackppo_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACT_LDS) !=
+      hipSuccess)
+    return false;
   g_policy_attr = true;
   return true;
 }
@@ -970,8 +1041,8 @@ int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env
   if (n_env == 0) return ACKPPO_OK;
   ActArgs A{params, obs_soa, n_env, env_offset, seed, step, deterministic, obs_rows, action, env_action, log_prob, value};
   if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_act: cannot reserve the policy LDS tile");
-  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS), sizeof(PolicyLds),
-                     (hipStream_t)stream, A);
+  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + AE - 1) / AE), dim3(GRAD_THREADS), ACT_LDS, (hipStream_t)stream,
+                     A);
   return launched("ackppo_act");
 }
 
