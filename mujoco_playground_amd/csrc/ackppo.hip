@@ -383,20 +383,43 @@ constexpr int GRAD_THREADS = 256;
 constexpr int GRAD_MAX_BLOCKS = 256;  // one workgroup per CU (the LDS footprint allows one)
 
 __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, float* w) {
-  // transposed first layers, both nets side by side (k row 79 = 0): coalesced global reads of
-  // the row-major [unit][79] weights, several loads in flight per thread (a strided read loop
-  // with one load outstanding cost 24k cycles per workgroup), transposed LDS writes
+  // Every global load of the staging is issued before the first LDS write (W1, W2 as 16-B loads,
+  // the short vectors as words), so a workgroup pays one memory latency instead of one per
+  // phase. First layers transposed (k row 79 = 0) and swizzled, second layers swizzled. (A
+  // conflict-free LDS -> LDS transpose through a scratch tile measured slower: 14.4k -> 20.2k
+  // cycles per workgroup.)
   static_assert(ACKPPO_OFF_PI_W1 % 4 == 0 && ACKPPO_OFF_VF_W1 % 4 == 0 && (H * NOBS) % 4 == 0, "16-B W1 staging");
+  static_assert(ACKPPO_OFF_PI_W2 % 4 == 0 && ACKPPO_OFF_VF_W2 % 4 == 0, "16-B W2 loads");
   constexpr int N1 = H * NOBS / 4, IT1 = (2 * N1 + GRAD_THREADS - 1) / GRAD_THREADS;  // float4 per net, 10 per thread
-  float4 v[IT1];
+  constexpr int IT2 = H * H / 4 / GRAD_THREADS;
+  const int tid = threadIdx.x;
+  float4 v[IT1], va[IT2], vc[IT2];
 #pragma unroll
-  for (int j = 0; j < IT1; j++) {  // all loads in flight first (16 B per lane)
-    const int i = threadIdx.x + j * GRAD_THREADS, net = i >= N1;
+  for (int j = 0; j < IT1; j++) {
+    const int i = tid + j * GRAD_THREADS, net = i >= N1;
     if (i < 2 * N1) v[j] = reinterpret_cast<const float4*>(p + (net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1))[i - net * N1];
   }
 #pragma unroll
+  for (int j = 0; j < IT2; j++) {
+    va[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_PI_W2)[tid + j * GRAD_THREADS];
+    vc[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_VF_W2)[tid + j * GRAD_THREADS];
+  }
+  // short vectors: thread t < 64 takes entry t of the 7 64-vectors; threads 64-68 the scalars
+  constexpr int VSRC[7] = {ACKPPO_OFF_PI_B1, ACKPPO_OFF_PI_B2, ACKPPO_OFF_VF_B1, ACKPPO_OFF_VF_B2,
+                           ACKPPO_OFF_ACT_W, ACKPPO_OFF_ACT_W + H, ACKPPO_OFF_VAL_W};
+  constexpr int VDST[7] = {W_B1_A, W_B2_A, W_B1_C, W_B2_C, W_AW, W_AW + H, W_CW};
+  float vs[7];
+  if (tid < H) {
+#pragma unroll
+    for (int j = 0; j < 7; j++) vs[j] = p[VSRC[j] + tid];
+  }
+  const int sc = tid - H;  // 0: act_b[0], 1: act_b[1], 2: log_std[0], 3: log_std[1], 4: val_b
+  const bool has_sc = sc >= 0 && sc < 5;
+  const float vsc = has_sc ? p[sc < 2 ? ACKPPO_OFF_ACT_B + sc : (sc < 4 ? ACKPPO_OFF_LOG_STD + sc - 2 : ACKPPO_OFF_VAL_B)]
+                           : 0.0f;
+#pragma unroll
   for (int j = 0; j < IT1; j++) {
-    const int i = threadIdx.x + j * GRAD_THREADS, net = i >= N1;
+    const int i = tid + j * GRAD_THREADS, net = i >= N1;
     if (i < 2 * N1) {
       const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
@@ -406,42 +429,22 @@ __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, 
       }
     }
   }
-  if (threadIdx.x < 2 * H) w[w1t_at(NOBS, threadIdx.x)] = 0.0f;
-  static_assert(ACKPPO_OFF_PI_W2 % 4 == 0 && ACKPPO_OFF_VF_W2 % 4 == 0, "16-B W2 loads");
-  {
-    constexpr int IT2 = H * H / 4 / GRAD_THREADS;
-    float4 va[IT2], vc[IT2];
+  if (tid < 2 * H) w[w1t_at(NOBS, tid)] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < IT2; j++) {
-      const int i = threadIdx.x + j * GRAD_THREADS;
-      va[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_PI_W2)[i];
-      vc[j] = reinterpret_cast<const float4*>(p + ACKPPO_OFF_VF_W2)[i];
-    }
+  for (int j = 0; j < IT2; j++) {
+    const int i = 4 * (tid + j * GRAD_THREADS), u = i / H, k = i - u * H;  // 4 k of one row
+    const float ea[4] = {va[j].x, va[j].y, va[j].z, va[j].w}, ec[4] = {vc[j].x, vc[j].y, vc[j].z, vc[j].w};
 #pragma unroll
-    for (int j = 0; j < IT2; j++) {
-      const int i = 4 * (threadIdx.x + j * GRAD_THREADS), u = i / H, k = i - u * H;  // 4 k of one row
-      const float ea[4] = {va[j].x, va[j].y, va[j].z, va[j].w}, ec[4] = {vc[j].x, vc[j].y, vc[j].z, vc[j].w};
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        w[W_W2_A + w2_at(u, k + c)] = ea[c];
-        w[W_W2_C + w2_at(u, k + c)] = ec[c];
-      }
+    for (int c = 0; c < 4; c++) {
+      w[W_W2_A + w2_at(u, k + c)] = ea[c];
+      w[W_W2_C + w2_at(u, k + c)] = ec[c];
     }
   }
-  for (int i = threadIdx.x; i < H; i += GRAD_THREADS) {
-    w[W_B1_A + i] = p[ACKPPO_OFF_PI_B1 + i];
-    w[W_B2_A + i] = p[ACKPPO_OFF_PI_B2 + i];
-    w[W_B1_C + i] = p[ACKPPO_OFF_VF_B1 + i];
-    w[W_B2_C + i] = p[ACKPPO_OFF_VF_B2 + i];
-    w[W_AW + i] = p[ACKPPO_OFF_ACT_W + i];
-    w[W_AW + H + i] = p[ACKPPO_OFF_ACT_W + H + i];
-    w[W_CW + i] = p[ACKPPO_OFF_VAL_W + i];
+  if (tid < H) {
+#pragma unroll
+    for (int j = 0; j < 7; j++) w[VDST[j] + tid] = vs[j];
   }
-  if (threadIdx.x < 2) {
-    w[W_AB + threadIdx.x] = p[ACKPPO_OFF_ACT_B + threadIdx.x];
-    w[W_LS + threadIdx.x] = p[ACKPPO_OFF_LOG_STD + threadIdx.x];
-  }
-  if (threadIdx.x == 0) w[W_CB] = p[ACKPPO_OFF_VAL_B];
+  if (has_sc) w[sc < 2 ? W_AB + sc : (sc < 4 ? W_LS + sc - 2 : W_CB)] = vsc;
 }
 
 __device__ __forceinline__ float row_sum_g(const float* a) {
