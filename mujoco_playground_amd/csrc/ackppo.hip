@@ -4,18 +4,18 @@
 // (hyper-parameters: the rl_logs/ppo checkpoints' data file). Network: 79-64-64 tanh actor and critic MLPs.
 //
 // Mapping:
-//  * rollout (ackppo_act / ackppo_value / ackppo_bootstrap): one lane per env, 64-lane
-//    workgroups; weights are read with wave-uniform addresses (scalar loads through the
-//    constant cache, FMA with an SGPR operand), hidden activations live in a per-lane LDS
-//    column so the unit loop stays rolled.
-//  * update (ackppo_grad): one 256-lane workgroup per 64-sample tile, lane = sample. Waves 0-1
-//    run the actor, waves 2-3 the critic, each on half of the hidden units: forward, loss
-//    gradient, backward to the hidden layers, all activations/deltas staged in LDS tiles
-//    [unit][sample]. All four waves then form
-//    the weight gradients (sums over the tile of outer products) as 4x4 register blocks fed
-//    by 16-B LDS reads along the sample axis, and write the tile's partial gradient row.
+//  * ackppo_act: 16 envs per 256-lane workgroup; weights staged in LDS (W1 transposed, both
+//    layers XOR-swizzled), both layers as 16x16 f32 MFMA tiles (v_mfma_f32_16x16x4_f32; wave w
+//    owns unit tiles 2w, 2w+1 of the 128 actor|critic units), heads + sampling on wave 0.
+//  * ackppo_value / ackppo_bootstrap: lane = env, 64 envs x 16 waves, the waves split the
+//    hidden units (VALU, LDS-broadcast weights).
+//  * ackppo_grad: one 256-lane workgroup per 32-sample tile. Forward layers, the W2^T backward
+//    and the weight-gradient sums over the tile (kept in the MFMA accumulators across tiles)
+//    are f32 MFMA tiles; heads, loss gradient and d2 on the VALU; every activation / delta
+//    lives in LDS tiles [unit][sample]. Each workgroup writes one partial gradient row.
 //    ackppo_reduce sums the rows (coalesced over parameters); ackppo_adam applies the global
-//    norm clip and the Adam step. The whole minibatch is 3 launches, no host round trip.
+//    norm clip and the Adam step; ackppo_epoch runs a whole epoch of minibatches in one host
+//    call. No host round trip inside an update.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>

@@ -1,12 +1,9 @@
 #!/bin/bash
-# r01f GPU probe: PPO kernel builds (event-timed), grad stamps, PPO GPU tests, bench (no CPU leg).
+# r01f GPU probe: step-kernel stamps (lane + quad), PPO kernel timing + grad stamps.
 set -o pipefail
 V=mujoco_playground_amd/csrc/build/variants
 mkdir -p gpurun_out
-timeout -k 10 200 python -u -m pytest tests/test_gpu_ppo.py -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_ppo.log 2>&1
-rc=$?
-[ $rc -le 1 ] || exit $rc
-timeout -k 10 120 python -u tools/ppo_kbench.py $V/libackppo_st3.so $V/libackppo_st5.so > gpurun_out/kbench.log 2>&1 &&
-timeout -k 10 60 python -u tools/ppo_kbench.py --stamps $V/libackppo_stamps.so >> gpurun_out/kbench.log 2>&1 || exit 1
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --no-cpu > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 120 python -u tools/stamps.py > gpurun_out/r01f_stamps_lane.txt 2>&1 &&
+timeout -k 10 120 python -u tools/stamps.py quad > gpurun_out/r01f_stamps_quad.txt 2>&1 &&
+timeout -k 10 120 python -u tools/ppo_kbench.py mujoco_playground_amd/csrc/build/libackppo.so > gpurun_out/r01f_ppo_kbench.txt 2>&1 &&
+timeout -k 10 60 python -u tools/ppo_kbench.py --stamps $V/libackppo_stamps.so >> gpurun_out/r01f_ppo_kbench.txt 2>&1
