@@ -101,7 +101,7 @@ def main():
     st = np.zeros((n, 44))
     o.reset(st, seed=3)
     rng = np.random.default_rng(0)
-    rules = [("exact", 0.0), ("warm", 0.0), ("smooth", 0.0)] + [("cap", t) for t in (3, 4, 5)]
+    rules = [("exact", 0.0), ("warm", 0.0), ("smooth", 0.0)]
     its = {r: [] for r in rules}
     errs = {r: [] for r in rules}
     for k in range(a.steps):
@@ -142,6 +142,12 @@ def main():
             for r in rules:
                 its[r].append(row_its[r])
         o.step(st, act, flags=FLAG_CONTACTS | FLAG_AUTORESET, seed=3)
+    # dual start: the iterations a solver racing both starts would need (the first to converge)
+    mn = np.concatenate([np.minimum(a, b) for a, b in zip(its[("warm", 0.0)], its[("smooth", 0.0)])])
+    for g in (16, 8):
+        W = mn.reshape(-1, g).max(1)
+        print(f"race min(warm, smooth): mean it {mn.mean():.2f}  hist {np.bincount(mn, minlength=10)[:12]}  "
+              f"wave-max hist ({g} envs/wave) {np.bincount(W, minlength=10)[:12]}", flush=True)
     for r in rules:
         I = np.concatenate(its[r])
         W = np.concatenate([x.reshape(-1, 16).max(1) for x in its[r]])

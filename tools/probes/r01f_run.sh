@@ -1,9 +1,10 @@
 #!/bin/bash
-# r01f GPU probe: step-kernel stamps (lane + quad), PPO kernel timing + grad stamps.
+# r01f GPU probe: quad race variant sweep, then the full GPU suite + smoke on the product build.
 set -o pipefail
-V=mujoco_playground_amd/csrc/build/variants
 mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/stamps.py > gpurun_out/r01f_stamps_lane.txt 2>&1 &&
-timeout -k 10 120 python -u tools/stamps.py quad > gpurun_out/r01f_stamps_quad.txt 2>&1 &&
-timeout -k 10 120 python -u tools/ppo_kbench.py mujoco_playground_amd/csrc/build/libackppo.so > gpurun_out/r01f_ppo_kbench.txt 2>&1 &&
-timeout -k 10 60 python -u tools/ppo_kbench.py --stamps $V/libackppo_stamps.so >> gpurun_out/r01f_ppo_kbench.txt 2>&1
+bash tools/variant_sweep.sh qbase qrace > gpurun_out/sweep.txt 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_race.txt 2>&1
+rc=$?
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_race.txt 2>&1
+exit $(( rc > 0 ? rc : $? ))
