@@ -368,7 +368,12 @@ constexpr int GT = 32, GLDP = 36;
 // (w1t_at / w2_at) so the MFMA operand reads -- 16 consecutive units x 4 consecutive k per wave --
 // hit 64 distinct LDS banks (W1T, layer-2 W2 reads) or at most 4 lanes per bank (W2^T reads).
 constexpr int W_W1T = 0, W_W2_A = 80 * 2 * H, W_W2_C = W_W2_A + H * H;
-__device__ __forceinline__ int w1t_at(int k, int c) { return W_W1T + k * 2 * H + (c ^ (16 * (k & 3))); }
+// W1T also XORs the unit index with (k >> 2) & 15: the staging writes, whose lanes hold
+// consecutive k of one unit, then spread over 16 banks instead of one (the reads stay
+// conflict-free: within a 16-unit block the extra XOR only permutes the units)
+__device__ __forceinline__ int w1t_at(int k, int c) {
+  return W_W1T + k * 2 * H + (c ^ (16 * (k & 3)) ^ ((k >> 2) & 15));
+}
 __device__ __forceinline__ int w2_at(int u, int k) { return u * H + (k ^ (4 * (u & 15))); }
 constexpr int W_B1_A = W_W2_C + H * H, W_B2_A = W_B1_A + H, W_B1_C = W_B2_A + H, W_B2_C = W_B1_C + H;
 constexpr int W_AW = W_B2_C + H, W_AB = W_AW + 2 * H, W_CW = W_AB + 4, W_CB = W_CW + H, W_LS = W_CB + 4;
@@ -571,7 +576,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll  // k0 compile-time: the W1T swizzle folds to an immediate XOR per read
       for (int k0 = 0; k0 < 80; k0 += 4) {
         const int k = k0 + lk;
         const float a0 = w[w1t_at(k, nid * H + ub0 + li)], a1 = w[w1t_at(k, nid * H + ub0 + 16 + li)];
@@ -834,7 +839,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
   const int nid = wave >> 1, ub0 = 32 * (wave & 1);
   {  // layer 1: [128 x 16] = W1T^T [128 x 80] . X [80 x 16]
     f4v acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 5
+#pragma unroll  // k0 compile-time: the W1T swizzle folds to an immediate XOR per read
     for (int k0 = 0; k0 < 80; k0 += 4) {
       const int k = k0 + lk;
       const float b = tl[A_X + k * AE + li];
