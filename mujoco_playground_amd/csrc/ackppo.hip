@@ -606,7 +606,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
       for (int k0 = 0; k0 < H; k0 += 4) {
         const int k = k0 + lk;
         const float a0 = W2[w2_at(ub0 + li, k)], a1 = W2[w2_at(ub0 + 16 + li, k)];
@@ -713,7 +713,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
       for (int k0 = 0; k0 < H; k0 += 4) {
         const int k = k0 + lk;  // layer-2 unit
         const float a0 = W2[w2_at(k, ub0 + li)], a1 = W2[w2_at(k, ub0 + 16 + li)];
@@ -739,7 +739,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     PSTAMP(6);
     // weight-gradient sums over the tile's samples (rows of padding samples are zero):
     // gW1 [units x 80] += D1 [units x 32] . X^T [32 x 80], gW2 [units x 64] += D2 . H1^T
-#pragma unroll 2
+#pragma unroll
     for (int q0 = 0; q0 < GT; q0 += 4) {
       const int q = q0 + lk;  // sample
       const float a0 = nt[G_D1 + (ub0 + li) * GLDP + q], a1 = nt[G_D1 + (ub0 + 16 + li) * GLDP + q];
@@ -859,7 +859,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
     const float* W2 = w + (nid ? W_W2_C : W_W2_A);
     const float* h1 = tl + A_H1 + nid * H * AE;
     f4v acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
     for (int k0 = 0; k0 < H; k0 += 4) {
       const int k = k0 + lk;
       const float b = h1[k * AE + li];
