@@ -1,10 +1,8 @@
 #!/bin/bash
-# r01f GPU probe: quad race variant sweep, then the full GPU suite + smoke on the product build.
+# r01f GPU probe: PPO kernel builds (event-timed), grad stamps, PPO GPU tests.
 set -o pipefail
+V=mujoco_playground_amd/csrc/build/variants
 mkdir -p gpurun_out
-bash tools/variant_sweep.sh qbase qrace > gpurun_out/sweep.txt 2>&1 || exit 1
-timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_race.txt 2>&1
-rc=$?
-[ $rc -le 1 ] || exit $rc
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_race.txt 2>&1
-exit $(( rc > 0 ? rc : $? ))
+timeout -k 10 120 python -u tools/ppo_kbench.py $V/libackppo_base.so $V/libackppo_pf.so > gpurun_out/kbench.txt 2>&1 &&
+timeout -k 10 60 python -u tools/ppo_kbench.py --stamps $V/libackppo_stamps.so >> gpurun_out/kbench.txt 2>&1 &&
+timeout -k 10 200 python -u -m pytest tests/test_gpu_ppo.py tests/test_gpu_obstacles.py -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_ppo.txt 2>&1
