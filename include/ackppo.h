@@ -89,6 +89,11 @@ int ackppo_gae(const float* rewards, const float* values, const float* episode_s
 int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int batch, int normalize,
                      float* stats, void* stream);
 
+/* out [n] = a keyed pseudo-random permutation of 0..n-1 (the minibatch shuffle of one epoch,
+ * SB3 rollout_buffer.get: np.random.permutation(buffer_size * n_envs)): a 4-round Feistel
+ * bijection with cycle walking, keyed by (seed, epoch); one launch, no sort. */
+int ackppo_permutation(int n, uint64_t seed, uint32_t epoch, int32_t* out, void* stream);
+
 /* Gradient of the PPO loss of one minibatch (samples idx[0..batch)), split over
  * nblk = ackppo_grad_blocks(batch) workgroups (one per CU at most), each writing its row of
  * grad_partial [nblk][NPARAM] (pad words are never written: zero them once) and of

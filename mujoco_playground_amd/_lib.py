@@ -66,7 +66,8 @@ EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackph
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
 PPO_EXPORTS = ["ackppo_act", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats", "ackppo_grad",
-               "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_last_error"]
+               "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_permutation",
+               "ackppo_last_error"]
 
 _lib = None
 _ppo = None
@@ -122,6 +123,7 @@ def ppo_lib():
     L.ackppo_grad_blocks.argtypes = [i32]
     L.ackppo_reduce.argtypes = [P, P, i32, f32, P, P, P]
     L.ackppo_adam.argtypes = [P, P, P, P, f32, f32, f32, f32, f32, f32, f32, P, P]
+    L.ackppo_permutation.argtypes = [i32, u64, u32, P, P]
     L.ackppo_epoch.argtypes = ([P] * 7 + [i32, i32, P, f32, f32, f32, f32, C.c_double, C.c_double, C.c_double, f32,
                                           i64] + [P] * 8)
     L.ackppo_last_error.restype = C.c_char_p

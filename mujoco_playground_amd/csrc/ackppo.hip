@@ -922,6 +922,38 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
   if (A.value) A.value[e] = val;
 }
 
+// ---- ackppo_permutation: out[i] = pi(i), a keyed pseudo-random bijection of [0, n) -- a
+// 4-round balanced Feistel network on 2*half >= bits(n - 1) bits (round function: a
+// multiply-xorshift hash of the right half and the round key), cycle-walked until the value
+// falls in [0, n) (bijective on [0, n) because the network is bijective on [0, 2^(2 half));
+// 2^(2 half) < 4n, so a walk takes < 4 network passes on average). One thread per index.
+__device__ __forceinline__ uint32_t perm_hash(uint32_t x, uint32_t k) {
+  x = (x ^ k) * 0x9E3779B1u;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  return x ^ (x >> 16);
+}
+extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int half, uint32_t k0, uint32_t k1,
+                                                                     uint32_t k2, uint32_t k3, int32_t* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t mask = (1u << half) - 1u, keys[4] = {k0, k1, k2, k3};
+  uint32_t x = (uint32_t)i;
+  do {
+    uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t t = L ^ (perm_hash(R, keys[r]) & mask);
+      L = R;
+      R = t;
+    }
+    x = (L << half) | R;
+  } while (x >= (uint32_t)n);
+  out[i] = (int32_t)x;
+}
+
 // Two passes, no atomics: (1) grid (param blocks of 256, REDUCE_RG row groups) sums rows
 // by, by + RG, ... into tmp[by][p] with 4 loads in flight per thread; (2) sums the RG rows.
 constexpr int REDUCE_RG = 16;
@@ -1085,6 +1117,27 @@ int ackppo_gae(const float* rewards, const float* values, const float* episode_s
   hipLaunchKernelGGL(ackppo_gae_kernel, dim3((n_env + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, values,
                      episode_starts, last_values, last_dones, T, n_env, gamma, gae_lambda, advantages, returns);
   return launched("ackppo_gae");
+}
+
+int ackppo_permutation(int n, uint64_t seed, uint32_t epoch, int32_t* out, void* stream) {
+  if (!out || n < 0 || n > (1 << 30)) return fail(ACKPPO_EINVAL, "ackppo_permutation: bad arguments");
+  if (n == 0) return ACKPPO_OK;
+  int bits = 1;
+  while ((1u << bits) < (uint32_t)n) bits++;
+  const int half = (bits + 1) / 2;
+  // round keys: splitmix64 of (seed, epoch)
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * ((uint64_t)epoch + 1));
+  uint32_t k[4];
+  for (int r = 0; r < 4; r++) {
+    z += 0x9E3779B97F4A7C15ull;
+    uint64_t y = z;
+    y = (y ^ (y >> 30)) * 0xBF58476D1CE4E5B9ull;
+    y = (y ^ (y >> 27)) * 0x94D049BB133111EBull;
+    k[r] = (uint32_t)(y ^ (y >> 31));
+  }
+  hipLaunchKernelGGL(ackppo_perm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, half, k[0], k[1],
+                     k[2], k[3], out);
+  return launched("ackppo_permutation");
 }
 
 int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int batch, int normalize, float* stats,

@@ -153,8 +153,10 @@ class PPO:
         self.gnorm = torch.zeros(1, **f32)
         nmb = (T * N + batch_size - 1) // batch_size
         self.mb_stats = torch.zeros(nmb, 2, **f32)
-        self.perm_gen = torch.Generator(device=dev)
-        self.perm_gen.manual_seed(self.seed * 7919 + self.rank)
+        # per-epoch minibatch shuffle: ackppo_permutation keyed by (seed, rank) and the epoch count
+        self.perm_key = (self.seed * 7919 + self.rank) & 0xFFFFFFFFFFFFFFFF
+        self.perm_epoch = 0
+        self.perm = torch.empty(self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
         self.num_timesteps = 0
         self.episodes_total = 0
         self._rollout_step = 0
@@ -231,7 +233,10 @@ class PPO:
         self.loss_acc.zero_()
         b1, b2 = 0.9, 0.999
         for _ in range(self.n_epochs):
-            perm = torch.randperm(S, device=self.device, generator=self.perm_gen).to(torch.int32)
+            _lib.ppo_check(L.ackppo_permutation(S, self.perm_key, self.perm_epoch, _ptr(self.perm), s),
+                           "ackppo_permutation")
+            self.perm_epoch += 1
+            perm = self.perm
             _lib.ppo_check(L.ackppo_adv_stats(_ptr(self.buf_adv), _ptr(perm), S, B, int(self.normalize_advantage),
                                               _ptr(self.mb_stats), s), "ackppo_adv_stats")
             if self.world == 1 and self.fused_epoch:  # one C call per epoch: grad -> reduce -> adam per minibatch

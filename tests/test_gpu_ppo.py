@@ -171,6 +171,64 @@ def test_ppo_learn_end_to_end():
     assert a.shape == (256, 2) and float(a.abs().max()) <= 1.0
 
 
+def _perm_ref(n, seed, epoch):
+    """Python restatement of ackppo_permutation (4-round Feistel + cycle walking)."""
+    M64, M32 = (1 << 64) - 1, (1 << 32) - 1
+    bits = 1
+    while (1 << bits) < n:
+        bits += 1
+    half = (bits + 1) // 2
+    z = (seed ^ (0x9E3779B97F4A7C15 * (epoch + 1))) & M64
+    keys = []
+    for _ in range(4):
+        z = (z + 0x9E3779B97F4A7C15) & M64
+        y = z
+        y = ((y ^ (y >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        y = ((y ^ (y >> 27)) * 0x94D049BB133111EB) & M64
+        keys.append((y ^ (y >> 31)) & M32)
+
+    def h(x, k):
+        x = ((x ^ k) * 0x9E3779B1) & M32
+        x ^= x >> 16
+        x = (x * 0x85EBCA6B) & M32
+        x ^= x >> 13
+        x = (x * 0xC2B2AE35) & M32
+        return x ^ (x >> 16)
+    mask = (1 << half) - 1
+    out = []
+    for i in range(n):
+        x = i
+        while True:
+            L, R = x >> half, x & mask
+            for k in keys:
+                L, R = R, L ^ (h(R, k) & mask)
+            x = (L << half) | R
+            if x < n:
+                break
+        out.append(x)
+    return np.array(out, np.int32)
+
+
+def test_permutation_kernel():
+    """ackppo_permutation: a bijection of 0..n-1, bit-exact with the Python restatement, keyed by
+    (seed, epoch)."""
+    for n in (1, 2, 3, 7, 1000, 4096, 100003, 131072):
+        out = torch.empty(n, dtype=torch.int32, device=DEV)
+        assert L().ackppo_permutation(n, 12345, 3, P(out), S()) == 0
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        np.testing.assert_array_equal(np.sort(o), np.arange(n))
+        if n <= 4096:
+            np.testing.assert_array_equal(o, _perm_ref(n, 12345, 3))
+    n = 131072
+    a, b, c = (torch.empty(n, dtype=torch.int32, device=DEV) for _ in range(3))
+    L().ackppo_permutation(n, 12345, 3, P(a), S())
+    L().ackppo_permutation(n, 12345, 4, P(b), S())
+    L().ackppo_permutation(n, 12346, 3, P(c), S())
+    torch.cuda.synchronize()
+    assert (a != b).float().mean().item() > 0.99 and (a != c).float().mean().item() > 0.99
+
+
 def test_fused_epoch_matches_per_minibatch_calls():
     """ackppo_epoch (one C call per epoch) and the per-minibatch grad/reduce/adam calls give
     bit-identical parameters, Adam moments and loss statistics."""
