@@ -21,7 +21,8 @@ PHASES = [(0, 1, "load+controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3
           (8, 9, "barriers"), (9, 10, "state store"), (11, 12, "obs wave: rays")]
 
 
-QUAD_PHASES = [(0, 5, "pre-newton"), (5, 6, "newton"), (6, 10, "post-newton")]
+QUAD_PHASES = [(0, 1, "load+controller"), (1, 2, "kinematics"), (2, 3, "M/bias/a0"), (3, 4, "contacts"),
+               (4, 5, "rows"), (5, 6, "newton"), (6, 10, "post-newton")]
 
 
 def main():
