@@ -302,41 +302,55 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_gae_kernel(const float*
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) ackppo_adv_stats_kernel(const float* adv, const int32_t* idx,
-                                                                          int n_idx, int batch, int normalize,
-                                                                          float* stats) {
-  __shared__ double red[256];
+// one 1024-lane workgroup per minibatch: the gathered advantages stay in registers (ADV_CACHE per
+// lane; larger minibatches re-gather the rest) for the two double-precision passes (mean, then
+// the unbiased variance about it), each reduced with wave shuffles and one LDS word per wave
+constexpr int ADV_THREADS = 1024, ADV_CACHE = 8;
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // red is reused between calls
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int i = 0; i < ADV_THREADS / 64; i++) t += red[i];
+  return t;
+}
+extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_stats_kernel(const float* adv, const int32_t* idx,
+                                                                                  int n_idx, int batch, int normalize,
+                                                                                  float* stats) {
+  __shared__ double red[ADV_THREADS / 64];
   const int m = blockIdx.x, tid = threadIdx.x;
   const int lo = m * batch, hi = min(lo + batch, n_idx), cnt = hi - lo;
   if (!normalize || cnt <= 1) {
     if (tid == 0) { stats[2 * m] = 0.0f; stats[2 * m + 1] = 1.0f; }
     return;
   }
+  float v[ADV_CACHE];
   double s = 0.0;
-#pragma unroll 8
-  for (int i = lo + tid; i < hi; i += 256) s += adv[idx[i]];
-  red[tid] = s;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
-    __syncthreads();
+#pragma unroll
+  for (int c = 0; c < ADV_CACHE; c++) {
+    const int i = lo + tid + c * ADV_THREADS;
+    v[c] = i < hi ? adv[idx[i]] : 0.0f;
+    s += v[c];
   }
-  const double mean = red[0] / cnt;
-  __syncthreads();
+  for (int i = lo + tid + ADV_CACHE * ADV_THREADS; i < hi; i += ADV_THREADS) s += adv[idx[i]];
+  const double mean = block_sum_d(s, red) / cnt;
   double q = 0.0;
-#pragma unroll 8
-  for (int i = lo + tid; i < hi; i += 256) {
+#pragma unroll
+  for (int c = 0; c < ADV_CACHE; c++) {
+    const double d = (double)v[c] - mean;
+    q += (lo + tid + c * ADV_THREADS < hi) ? d * d : 0.0;
+  }
+  for (int i = lo + tid + ADV_CACHE * ADV_THREADS; i < hi; i += ADV_THREADS) {
     const double d = adv[idx[i]] - mean;
     q += d * d;
   }
-  red[tid] = q;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
-    __syncthreads();
-  }
+  const double var = block_sum_d(q, red) / (cnt - 1);
   if (tid == 0) {
-    const float sd = (float)sqrt(red[0] / (cnt - 1));
+    const float sd = (float)sqrt(var);
     stats[2 * m] = (float)mean;
     stats[2 * m + 1] = 1.0f / (sd + 1e-8f);
   }
@@ -1145,7 +1159,7 @@ int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int
   if (!advantages || !idx || !stats || n_idx < 0 || batch <= 0) return fail(ACKPPO_EINVAL, "ackppo_adv_stats: bad arguments");
   const int nmb = (n_idx + batch - 1) / batch;
   if (nmb == 0) return ACKPPO_OK;
-  hipLaunchKernelGGL(ackppo_adv_stats_kernel, dim3(nmb), dim3(256), 0, (hipStream_t)stream, advantages, idx, n_idx,
+  hipLaunchKernelGGL(ackppo_adv_stats_kernel, dim3(nmb), dim3(ADV_THREADS), 0, (hipStream_t)stream, advantages, idx, n_idx,
                      batch, normalize, stats);
   return launched("ackppo_adv_stats");
 }

@@ -1,8 +1,6 @@
 #!/bin/bash
-# r01f GPU probe: PPO GPU tests, PPO kernel builds, bench without the CPU leg.
+# r01f GPU probe: PPO GPU tests, then the bench without the CPU leg.
 set -o pipefail
-V=mujoco_playground_amd/csrc/build/variants
 mkdir -p gpurun_out
 timeout -k 10 200 python -u -m pytest tests/test_gpu_ppo.py -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_ppo.txt 2>&1 &&
-timeout -k 10 120 python -u tools/ppo_kbench.py $V/libackppo_base.so $V/libackppo_fr.so > gpurun_out/kbench.txt 2>&1 &&
 timeout -k 10 300 python -u bench.py --no-cpu > gpurun_out/bench_nocpu.json 2> gpurun_out/bench_nocpu.err
