@@ -43,11 +43,20 @@ def algorithmic_bytes_per_env_step() -> int:
     return 176 + 8 + 16 + 152 + 316 + 4 + 2 + 16
 
 
+# With contacts the robot spawns 0.1 m above the floor (simple_map_spawner.py:43) and lands after
+# ~70 steps; until then a contacts-on step is a free-fall step. The contacts legs therefore run at
+# least SETTLE_STEPS untimed steps (the driver's short --warmup included) so the timed steps are
+# ground-contact steps whatever --warmup is.
+SETTLE_STEPS = 200
+
+
 def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat"):
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
                               env_offset=shard.env_offset(rank, n_env), variant=variant, scene=scene)
     sim.reset()
-    actions = sim.random_actions(warmup + steps, seed=seed)
+    pre = max(warmup, SETTLE_STEPS) if contacts else warmup
+    actions = sim.random_actions(pre + steps, seed=seed)
+    warmup = pre
     for k in range(warmup):
         sim.step(actions[k], want_info=False)
     stream = torch.cuda.current_stream(device)
@@ -239,7 +248,8 @@ def main():
     if not a.no_secondary:
         _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant)
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
-                     "kernel_ms": km2}
+                     "kernel_ms": km2,
+                     "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup}
     ppo = None if a.no_ppo else run_ppo(a.envs, rank, world, device)
     obstacles = None
     if not a.no_obstacles:
@@ -248,6 +258,7 @@ def main():
                                  "random ctrl, contacts enabled, spawn at the scene's free cell",
                      "value": total_envs * a.steps / el3, "unit": "env-steps/s", "ms_per_step": el3 * 1e3 / a.steps,
                      "kernel": "ackphys_step_obst_kernel", "kernel_ms": km3, "episodes": rets3,
+                     "untimed_steps": max(a.warmup, SETTLE_STEPS),
                      "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
     parity = base = None
     if rank == 0 and not a.no_cpu:

@@ -89,6 +89,20 @@ int ackppo_gae(const float* rewards, const float* values, const float* episode_s
 int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int batch, int normalize,
                      float* stats, void* stream);
 
+/* Data-parallel advantage statistics (a world minibatch m = the union of every rank's minibatch m,
+ * so all ranks normalise with the statistics of the whole world minibatch, as one SB3 learner
+ * with world x batch samples would). moments [3][nmb] float64, nmb = ceil(n_idx / batch):
+ *   phase 0: moments[0][m] = count, moments[1][m] = sum of this rank's advantages, moments[2][m] = 0;
+ *   (caller all-reduces rows 0..1 with SUM)
+ *   phase 1: moments[2][m] = sum of (a - mean_m)^2 about the global mean moments[1][m] / moments[0][m];
+ *   (caller all-reduces row 2 with SUM)
+ * then ackppo_adv_finalize: stats[m] = (mean, 1/(std+1e-8)), unbiased std over the world
+ * minibatch; (0, 1) when normalize == 0 or the world minibatch has one sample. At world 1 the
+ * three calls give ackppo_adv_stats' stats bit for bit. */
+int ackppo_adv_moments(const float* advantages, const int32_t* idx, int n_idx, int batch, int phase,
+                       double* moments, void* stream);
+int ackppo_adv_finalize(const double* moments, int nmb, int normalize, float* stats, void* stream);
+
 /* out [n] = a keyed pseudo-random permutation of 0..n-1 (the minibatch shuffle of one epoch,
  * SB3 rollout_buffer.get: np.random.permutation(buffer_size * n_envs)): a 4-round Feistel
  * bijection with cycle walking, keyed by (seed, epoch); one launch, no sort. */
@@ -109,8 +123,9 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
 int ackppo_grad_blocks(int batch);
 
 /* grad [NPARAM] = sum of nblk partial rows (grad is overwritten); d(-ent_coef * entropy)/d log_std = -ent_coef added;
- * loss [8] = column sums of loss_partial. */
-int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+ * loss [8] = column sums of loss_partial. grad_partial is CONSUMED: its first min(nblk, 16) rows are
+ * overwritten with row-group sums (no library-owned scratch; the next ackppo_grad rewrites every row). */
+int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream);
 
 /* clip_grad_norm_(max_grad_norm) + torch.optim.Adam step on grad * grad_scale (grad_scale =

@@ -7,21 +7,38 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
 import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(CSRC, "build", "libackphys.so")
 REPO = os.path.dirname(PKG)
-SOURCES = [os.path.join(CSRC, "ackphys_step.hip"), os.path.join(CSRC, "ackphys_quad.inc"),
-           os.path.join(CSRC, "ackphys_model_gen.h"),
-           os.path.join(REPO, "include", "ackphys.h"), os.path.join(REPO, "include", "ackphys_model.h")]
+_INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def source_closure(main: str) -> list:
+    """`main` plus every file it reaches through quoted #include lines (resolved relative to the
+    including file), so the rebuild check sees edits to any .inc / generated header."""
+    seen, todo = [], [os.path.abspath(main)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.append(f)
+        with open(f, encoding="utf-8", errors="replace") as fh:
+            for inc in _INCLUDE_RE.findall(fh.read()):
+                todo.append(os.path.normpath(os.path.join(os.path.dirname(f), inc)))
+    return seen
+
+
+SOURCES = source_closure(os.path.join(CSRC, "ackphys_step.hip"))
 BLOB_PATH = os.path.join(PKG, "model", "assets", "ackermann_robot_v2.apm")
 # static-world scenes the kernels are specialised on: "flat" = ackermann_robot_v2.xml alone,
 # "obstacles" = the v2 robot in models/environments/ackermann_maze_flat.xml (SURVEY §8f rank 2)
 SCENES = {"flat": BLOB_PATH, "obstacles": os.path.join(PKG, "model", "assets", "ackermann_obstacles.apm")}
 PPO_LIB_PATH = os.path.join(CSRC, "build", "libackppo.so")
-PPO_SOURCES = [os.path.join(CSRC, "ackppo.hip"), os.path.join(REPO, "include", "ackppo.h")]
+PPO_SOURCES = source_closure(os.path.join(CSRC, "ackppo.hip"))
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-fast-math",
                "-Wno-unused-result"]
@@ -65,7 +82,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
 EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
-PPO_EXPORTS = ["ackppo_act", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats", "ackppo_grad",
+PPO_EXPORTS = ["ackppo_act", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
+               "ackppo_adv_moments", "ackppo_adv_finalize", "ackppo_grad",
                "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_permutation",
                "ackppo_last_error"]
 
@@ -119,6 +137,8 @@ def ppo_lib():
     L.ackppo_bootstrap.argtypes = [P, P, P, P, P, i32, f32, P, P, P]
     L.ackppo_gae.argtypes = [P, P, P, P, P, i32, i32, f32, f32, P, P, P]
     L.ackppo_adv_stats.argtypes = [P, P, i32, i32, i32, P, P]
+    L.ackppo_adv_moments.argtypes = [P, P, i32, i32, i32, P, P]
+    L.ackppo_adv_finalize.argtypes = [P, i32, i32, P, P]
     L.ackppo_grad.argtypes = [P, P, P, P, P, P, P, i32, P, f32, f32, f32, P, P, P]
     L.ackppo_grad_blocks.argtypes = [i32]
     L.ackppo_reduce.argtypes = [P, P, i32, f32, P, P, P]

@@ -1891,6 +1891,21 @@ static int hipfail(hipError_t e, const char* where) {
   return ACKPHYS_EHIP;
 }
 
+// Switches the calling thread to the context's device only when it differs, and restores the
+// caller's device on return (torch keeps its own notion of the current device).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 static uint64_t fnv1a64(const unsigned char* p, size_t n) {
   uint64_t h = 0xCBF29CE484222325ull;
   for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 0x100000001B3ull; }
@@ -1977,8 +1992,9 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
                  void* stream) {
   if (!ctx || !action || !state || !obs || !reward || !term || !trunc)
     return fail(ACKPHYS_EINVAL, "ackphys_step: NULL argument");
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  DeviceGuard dg(ctx->device);
+  if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
+  hipError_t e;
   ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
              ctx->env_offset, 64};
   // AUTO: with contacts the quad mapping wins (contact rows dominate and split 4 ways); without
@@ -2016,8 +2032,9 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
 
 int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* state, float* obs, void* stream) {
   if (!ctx || !state || !obs) return fail(ACKPHYS_EINVAL, "ackphys_reset: NULL argument");
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  DeviceGuard dg(ctx->device);
+  if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
+  hipError_t e;
   int blocks = (ctx->n_env + 255) / 256;
   if (ctx->scene == 1)
     hipLaunchKernelGGL(ackphys_reset_obst_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, mask, state, obs,
@@ -2032,8 +2049,9 @@ int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* sta
 
 int ackphys_random_actions(ackphys_t* ctx, float* actions, int k_steps, uint64_t seed, uint32_t step0, void* stream) {
   if (!ctx || !actions || k_steps <= 0) return fail(ACKPHYS_EINVAL, "ackphys_random_actions: bad argument");
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+  DeviceGuard dg(ctx->device);
+  if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
+  hipError_t e;
   int blocks = (ctx->n_env + 255) / 256;
   hipLaunchKernelGGL(ackphys_actions_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, actions, ctx->n_env,
                      k_steps, seed, step0, ctx->env_offset);

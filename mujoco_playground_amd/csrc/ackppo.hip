@@ -356,6 +356,56 @@ extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_stats_kerne
   }
 }
 
+// Data-parallel form of the same statistics (a world minibatch m is the union of every rank's
+// minibatch m): phase 0 writes this rank's (count, sum) into moments[0..1][m]; after the host
+// all-reduces those rows, phase 1 writes the squared deviations about the GLOBAL mean into
+// moments[2][m]; after the second all-reduce, ackppo_adv_finalize forms the stats. The sums are
+// the single-rank kernel's, so world 1 reproduces ackppo_adv_stats bit for bit.
+extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_moments_kernel(const float* adv,
+                                                                                    const int32_t* idx, int n_idx,
+                                                                                    int batch, int phase, int nmb,
+                                                                                    double* moments) {
+  __shared__ double red[ADV_THREADS / 64];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int lo = m * batch, hi = min(lo + batch, n_idx), cnt = hi - lo;
+  if (phase == 0) {
+    double s = 0.0;
+    for (int i = lo + tid; i < hi; i += ADV_THREADS) s += adv[idx[i]];
+    // same per-lane order as ackppo_adv_stats_kernel: cached slots then the rest, all ascending
+    const double tot = block_sum_d(s, red);
+    if (tid == 0) {
+      moments[m] = (double)cnt;
+      moments[nmb + m] = tot;
+      moments[2 * nmb + m] = 0.0;
+    }
+  } else {
+    const double n = moments[m];
+    const double mean = n > 0.0 ? moments[nmb + m] / n : 0.0;
+    double q = 0.0;
+    for (int i = lo + tid; i < hi; i += ADV_THREADS) {
+      const double d = (double)adv[idx[i]] - mean;
+      q += d * d;
+    }
+    const double tot = block_sum_d(q, red);
+    if (tid == 0) moments[2 * nmb + m] = tot;
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) ackppo_adv_finalize_kernel(const double* moments, int nmb,
+                                                                             int normalize, float* stats) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= nmb) return;
+  const double n = moments[m];
+  if (!normalize || n <= 1.0) {
+    stats[2 * m] = 0.0f;
+    stats[2 * m + 1] = 1.0f;
+    return;
+  }
+  const double mean = moments[nmb + m] / n;
+  const float sd = (float)sqrt(moments[2 * nmb + m] / (n - 1.0));
+  stats[2 * m] = (float)mean;
+  stats[2 * m + 1] = 1.0f / (sd + 1e-8f);
+}
+
 // ------------------------------------------------------------------ update kernels
 
 struct GradArgs {
@@ -968,10 +1018,13 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int 
   out[i] = (int32_t)x;
 }
 
-// Two passes, no atomics: (1) grid (param blocks of 256, REDUCE_RG row groups) sums rows
-// by, by + RG, ... into tmp[by][p] with 4 loads in flight per thread; (2) sums the RG rows.
+// Two passes, no atomics, no scratch: (1) grid (param blocks of 256, RG row groups) sums rows
+// by, by + RG, ... with 4 loads in flight per thread and writes the sum IN PLACE into row by
+// (row by belongs to group by alone, and element (by, p) to one thread, which read it first);
+// (2) sums rows 0..RG-1. The caller-owned partial rows are the only buffer, so concurrent
+// learners on other streams or devices share nothing.
 constexpr int REDUCE_RG = 16;
-extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(const float* gpart, int nblk, float* tmp) {
+extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(float* gpart, int nblk) {
   const int pidx = blockIdx.x * 256 + threadIdx.x;
   const int rg = gridDim.y, by = blockIdx.y;
   if (pidx >= P) return;
@@ -982,7 +1035,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(cons
     for (int i = 0; i < 4; i++) acc[i] += gpart[(size_t)(b + i * rg) * P + pidx];
   }
   for (; b < nblk; b += rg) acc[0] += gpart[(size_t)b * P + pidx];
-  tmp[(size_t)by * P + pidx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  gpart[(size_t)by * P + pidx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const float* tmp, int rg, const float* lpart,
                                                                        int nblk, float ent_coef, float* grad,
@@ -1062,11 +1115,18 @@ int launched(const char* what) {
   return ACKPPO_OK;
 }
 constexpr size_t GRAD_LDS = (size_t)G_TOTAL * sizeof(float);
-bool g_grad_attr = false;
-float* g_reduce_tmp = nullptr;  // [REDUCE_RG][NPARAM] row-group sums (one small scratch per process)
-bool g_policy_attr = false;
+// hipFuncSetAttribute is applied per device: flags indexed by the caller's current device
+constexpr int MAX_DEV = 64;
+bool g_grad_attr[MAX_DEV] = {};
+bool g_policy_attr[MAX_DEV] = {};
+int current_device() {
+  int d = 0;
+  return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < MAX_DEV) ? d : -1;
+}
 bool policy_lds_ready() {
-  if (g_policy_attr) return true;
+  const int dev = current_device();
+  if (dev < 0) return false;
+  if (g_policy_attr[dev]) return true;
   const void* ks[2] = {(const void*)ackppo_value_kernel, (const void*)ackppo_bootstrap_kernel};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(PolicyLds)) != hipSuccess)
@@ -1074,7 +1134,7 @@ bool policy_lds_ready() {
   if (hipFuncSetAttribute((const void*)ackppo_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACT_LDS) !=
       hipSuccess)
     return false;
-  g_policy_attr = true;
+  g_policy_attr[dev] = true;
   return true;
 }
 }  // namespace
@@ -1164,6 +1224,25 @@ int ackppo_adv_stats(const float* advantages, const int32_t* idx, int n_idx, int
   return launched("ackppo_adv_stats");
 }
 
+int ackppo_adv_moments(const float* advantages, const int32_t* idx, int n_idx, int batch, int phase, double* moments,
+                       void* stream) {
+  if (!advantages || !idx || !moments || n_idx < 0 || batch <= 0 || (phase != 0 && phase != 1))
+    return fail(ACKPPO_EINVAL, "ackppo_adv_moments: bad arguments");
+  const int nmb = (n_idx + batch - 1) / batch;
+  if (nmb == 0) return ACKPPO_OK;
+  hipLaunchKernelGGL(ackppo_adv_moments_kernel, dim3(nmb), dim3(ADV_THREADS), 0, (hipStream_t)stream, advantages, idx,
+                     n_idx, batch, phase, nmb, moments);
+  return launched("ackppo_adv_moments");
+}
+
+int ackppo_adv_finalize(const double* moments, int nmb, int normalize, float* stats, void* stream) {
+  if (!moments || !stats || nmb < 0) return fail(ACKPPO_EINVAL, "ackppo_adv_finalize: bad arguments");
+  if (nmb == 0) return ACKPPO_OK;
+  hipLaunchKernelGGL(ackppo_adv_finalize_kernel, dim3((nmb + 255) / 256), dim3(256), 0, (hipStream_t)stream, moments,
+                     nmb, normalize, stats);
+  return launched("ackppo_adv_finalize");
+}
+
 int ackppo_grad(const float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
                 const float* advantages, const float* returns, const int32_t* idx, int batch, const float* stats,
                 float clip_range, float ent_coef, float vf_coef, float* grad_partial, float* loss_partial,
@@ -1171,11 +1250,13 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
   if (!params || !obs_rows || !actions || !old_log_prob || !advantages || !returns || !idx || !stats ||
       !grad_partial || !loss_partial || batch <= 0)
     return fail(ACKPPO_EINVAL, "ackppo_grad: bad arguments");
-  if (!g_grad_attr) {
+  const int dev = current_device();
+  if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
+  if (!g_grad_attr[dev]) {
     const hipError_t e = hipFuncSetAttribute((const void*)ackppo_grad_kernel,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS);
     if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the 158 KiB LDS footprint");
-    g_grad_attr = true;
+    g_grad_attr[dev] = true;
   }
   GradArgs A{params, obs_rows, actions, old_log_prob, advantages, returns, idx, batch, stats, clip_range, ent_coef,
              vf_coef, grad_partial, loss_partial};
@@ -1191,20 +1272,18 @@ int ackppo_grad_blocks(int batch) {
 }
 
 namespace {
-int reduce_launch(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+int reduce_launch(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, int accumulate, void* stream) {
   const int rg = nblk < REDUCE_RG ? nblk : REDUCE_RG;
-  if (!g_reduce_tmp && hipMalloc(&g_reduce_tmp, sizeof(float) * P * REDUCE_RG) != hipSuccess)
-    return fail(ACKPPO_EHIP, "ackppo_reduce: scratch allocation");
   hipLaunchKernelGGL(ackppo_reduce_rows_kernel, dim3((P + 255) / 256, rg), dim3(256), 0, (hipStream_t)stream,
-                     grad_partial, nblk, g_reduce_tmp);
-  hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, g_reduce_tmp, rg,
+                     grad_partial, nblk);
+  hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, grad_partial, rg,
                      loss_partial, nblk, ent_coef, grad, loss, accumulate);
   return launched("ackppo_reduce");
 }
 }  // namespace
 
-int ackppo_reduce(const float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
+int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream) {
   if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0) return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments");
   return reduce_launch(grad_partial, loss_partial, nblk, ent_coef, grad, loss, 0, stream);

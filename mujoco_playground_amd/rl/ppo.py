@@ -8,16 +8,19 @@ libackppo.so (include/ackppo.h) on the GPU, next to the env step:
   rollout step : ackppo_act (policy -> action, log_prob, value, obs row)  -> ackphys_step
                  (auto-reset) -> ackppo_bootstrap (TimeLimit bootstrap, done flags)
   after rollout: ackppo_value (last values) -> ackppo_gae
-  each epoch   : one device permutation, ackppo_adv_stats for all minibatches
+  each epoch   : one device permutation (ackppo_permutation, the SB3 minibatch shuffle),
+                 advantage statistics for all minibatches (ackppo_adv_stats)
   minibatch    : ackppo_grad -> ackppo_reduce -> [RCCL all-reduce of 75 KB] -> ackppo_adam
 
 Nothing leaves the device inside `learn` except the logging scalars at the end of an update.
-Torch tensors are the buffer container only (and `torch.randperm` the shuffle).
+Torch tensors are the buffer container only.
 
 Data-parallel (one process per GPU, torchrun): every rank steps its own env shard (env_offset
 = rank * n_envs), parameters are broadcast from rank 0 once, and each minibatch gradient is
 summed over ranks with one all-reduce; the Adam kernel scales by 1/world. A minibatch is then
-world x batch_size samples, split evenly over ranks.
+world x batch_size samples, split evenly over ranks, and its advantages are normalised with the
+statistics of all world x batch_size samples (ackppo_adv_moments: two small all-reduces of the
+per-minibatch count / sum / squared deviations per epoch), as one SB3 learner would.
 """
 from __future__ import annotations
 
@@ -153,6 +156,7 @@ class PPO:
         self.gnorm = torch.zeros(1, **f32)
         nmb = (T * N + batch_size - 1) // batch_size
         self.mb_stats = torch.zeros(nmb, 2, **f32)
+        self.mb_moments = torch.zeros(3, nmb, dtype=torch.float64, device=dev)  # DP advantage statistics
         # per-epoch minibatch shuffle: ackppo_permutation keyed by (seed, rank) and the epoch count
         self.perm_key = (self.seed * 7919 + self.rank) & 0xFFFFFFFFFFFFFFFF
         self.perm_epoch = 0
@@ -237,8 +241,7 @@ class PPO:
                            "ackppo_permutation")
             self.perm_epoch += 1
             perm = self.perm
-            _lib.ppo_check(L.ackppo_adv_stats(_ptr(self.buf_adv), _ptr(perm), S, B, int(self.normalize_advantage),
-                                              _ptr(self.mb_stats), s), "ackppo_adv_stats")
+            self._advantage_stats(perm, S, B)
             if self.world == 1 and self.fused_epoch:  # one C call per epoch: grad -> reduce -> adam per minibatch
                 _lib.ppo_check(L.ackppo_epoch(_ptr(self.params), _ptr(self.buf_obs), _ptr(self.buf_act),
                                               _ptr(self.buf_logp), _ptr(self.buf_adv), _ptr(self.buf_ret), _ptr(perm),
@@ -274,6 +277,21 @@ class PPO:
                        "train/entropy_loss": -float((0.5 + 0.5 * math.log(2 * math.pi) + log_std).sum()),
                        "train/std": float(log_std.exp().mean()), "train/n_updates": self.adam_step,
                        "train/grad_norm": float(self.gnorm.item())}
+
+    def _advantage_stats(self, perm, S: int, B: int):
+        """mb_stats[m] = (mean, 1/(std+1e-8)) of world minibatch m (SB3 normalize_advantage)."""
+        L, s = self.L, self._stream()
+        if self.world == 1:
+            _lib.ppo_check(L.ackppo_adv_stats(_ptr(self.buf_adv), _ptr(perm), S, B, int(self.normalize_advantage),
+                                              _ptr(self.mb_stats), s), "ackppo_adv_stats")
+            return
+        mom = self.mb_moments
+        _lib.ppo_check(L.ackppo_adv_moments(_ptr(self.buf_adv), _ptr(perm), S, B, 0, _ptr(mom), s), "ackppo_adv_moments")
+        shard.all_reduce_sum_(mom[0:2], self.world)
+        _lib.ppo_check(L.ackppo_adv_moments(_ptr(self.buf_adv), _ptr(perm), S, B, 1, _ptr(mom), s), "ackppo_adv_moments")
+        shard.all_reduce_sum_(mom[2], self.world)
+        _lib.ppo_check(L.ackppo_adv_finalize(_ptr(mom), mom.shape[1], int(self.normalize_advantage),
+                                             _ptr(self.mb_stats), s), "ackppo_adv_finalize")
 
     def learn(self, total_timesteps: int, callback=None, log_interval: int = 1, reset_num_timesteps: bool = True,
               progress_bar: bool = False):

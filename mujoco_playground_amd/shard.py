@@ -48,8 +48,8 @@ def env_offset(rank: int, envs_per_rank: int) -> int:
 def gather_episode_stats(episode: torch.Tensor, world: int) -> torch.Tensor:
     """episode [4, n] (running return, running length, completed-return sum, completed count)
     -> [world, 4, n] on every rank (one all_gather_into_tensor)."""
-    if world == 1:
-        return episode.unsqueeze(0).clone()
+    if world == 1:  # nothing to exchange: a view, no copy launch inside a timed region
+        return episode.unsqueeze(0)
     src = episode.contiguous()
     if _backend_is_gloo() and src.is_cuda:
         src = src.cpu()

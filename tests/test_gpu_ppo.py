@@ -229,6 +229,53 @@ def test_permutation_kernel():
     assert (a != b).float().mean().item() > 0.99 and (a != c).float().mean().item() > 0.99
 
 
+def _moments_stats(adv_list, idx_list, n_idx, batch, normalize=1):
+    """The data-parallel statistics path with the all-reduces done on the host: one moments
+    buffer per 'rank', rows 0..1 summed after phase 0 and row 2 after phase 1."""
+    nmb = (n_idx + batch - 1) // batch
+    moms = [torch.zeros(3, nmb, dtype=torch.float64, device=DEV) for _ in adv_list]
+    for a, i, m in zip(adv_list, idx_list, moms):
+        assert L().ackppo_adv_moments(P(a), P(i), n_idx, batch, 0, P(m), S()) == 0
+    tot = sum(m[0:2] for m in moms)
+    for m in moms:
+        m[0:2].copy_(tot)
+    for a, i, m in zip(adv_list, idx_list, moms):
+        assert L().ackppo_adv_moments(P(a), P(i), n_idx, batch, 1, P(m), S()) == 0
+    tot2 = sum(m[2] for m in moms)
+    stats = torch.zeros(nmb, 2, device=DEV)
+    moms[0][2].copy_(tot2)
+    assert L().ackppo_adv_finalize(P(moms[0]), nmb, normalize, P(stats), S()) == 0
+    torch.cuda.synchronize()
+    return stats.cpu().numpy()
+
+
+@pytest.mark.parametrize("n_idx,batch", [(5000, 1000), (20000, 8192), (9, 1), (70000, 65536)])
+def test_adv_moments_world1_equals_adv_stats(n_idx, batch):
+    """At world 1 the data-parallel statistics path reproduces ackppo_adv_stats bit for bit."""
+    rng = np.random.default_rng(n_idx)
+    adv = torch.tensor(rng.normal(0.4, 3.0, n_idx).astype(np.float32), device=DEV)
+    idx = torch.tensor(rng.permutation(n_idx).astype(np.int32), device=DEV)
+    nmb = (n_idx + batch - 1) // batch
+    ref = torch.zeros(nmb, 2, device=DEV)
+    assert L().ackppo_adv_stats(P(adv), P(idx), n_idx, batch, 1, P(ref), S()) == 0
+    np.testing.assert_array_equal(_moments_stats([adv], [idx], n_idx, batch), ref.cpu().numpy())
+
+
+def test_adv_moments_two_ranks_normalise_the_world_minibatch():
+    """Two ranks' minibatch m together form the world minibatch; the statistics are those of the
+    union (mean and unbiased std in float64), as one SB3 learner with 2 x batch samples."""
+    rng = np.random.default_rng(5)
+    n_idx, batch = 6000, 1500
+    advs = [rng.normal(mu, sd, n_idx).astype(np.float32) for mu, sd in ((0.0, 1.0), (2.0, 4.0))]
+    idxs = [rng.permutation(n_idx).astype(np.int32) for _ in advs]
+    got = _moments_stats([torch.tensor(a, device=DEV) for a in advs], [torch.tensor(i, device=DEV) for i in idxs],
+                         n_idx, batch)
+    for m in range(n_idx // batch):
+        u = np.concatenate([a[i[m * batch:(m + 1) * batch]].astype(np.float64) for a, i in zip(advs, idxs)])
+        np.testing.assert_allclose(got[m, 0], u.mean(), rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(got[m, 1], 1.0 / (u.std(ddof=1) + 1e-8), rtol=1e-6)
+
+
 def test_fused_epoch_matches_per_minibatch_calls():
     """ackppo_epoch (one C call per epoch) and the per-minibatch grad/reduce/adam calls give
     bit-identical parameters, Adam moments and loss statistics."""

@@ -80,6 +80,16 @@ def test_capi_exports_every_declared_symbol():
     assert L.ackphys_model_fnv() == blobmod.fnv1a64(_lib.load_blob())
 
 
+def test_rebuild_check_covers_every_included_source():
+    """The staleness check of _lib.build() sees every file the kernels #include (the obstacle-scene
+    .inc and generated headers included), so an edit to any of them triggers a rebuild."""
+    names = {os.path.basename(s) for s in _lib.SOURCES}
+    assert {"ackphys_step.hip", "ackphys_quad.inc", "ackphys_scene.inc", "ackphys_model_gen.h",
+            "ackphys_scene_gen.h", "ackphys.h", "ackphys_model.h"} <= names
+    assert os.path.basename(_lib.SOURCES[0]) == "ackphys_step.hip"
+    assert {os.path.basename(s) for s in _lib.PPO_SOURCES} == {"ackppo.hip", "ackppo.h"}
+
+
 def test_create_rejects_wrong_blob():
     L = _lib.lib()
     ctx = C.c_void_p()
