@@ -365,6 +365,9 @@ struct SymPat { bool nz[NV][NV]; };
 #ifndef AK_NC_WARMSTART
 #define AK_NC_WARMSTART 1  // contacts-off kernel: Newton starts from qacc_warmstart (see dynamics())
 #endif
+#ifndef AK_NC_PREDICT
+#define AK_NC_PREDICT 1  // contacts-off kernel: first solve on a predicted active set (see dynamics())
+#endif
 #define QUAD_K(k) (AK_QUAD_DENSE ? 3 : (k))
 #ifdef AK_ORD_IDENT
 constexpr int ORD[NV] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
@@ -1258,9 +1261,92 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       }
     }
   }
-  // scalar jar at a
+  // Predicted active set (contacts-off kernel). Within a fixed set of row states the cost is
+  // quadratic, so ONE Newton step from any point on that piece lands on its minimiser, and if the
+  // rows there are in the assumed states that minimiser is the optimum (strict convexity). The
+  // states are predicted from two points: qacc_smooth moved onto the steering equality (the servo
+  // drives one steer, the equality the other), which decides the rows it puts far from their
+  // friction-loss kinks (the actuated wheels and steers: |x| > 50 R floss), and qacc_warmstart
+  // for the rest (the unactuated front spins, which sit in the quadratic zone step after step).
+  // The f64 probe (tools/probes/active_set_probe.py) finds the exact final states this way for
+  // 99.35 % of env-steps on the benchmark workload; a miss continues with Newton from the piece's
+  // minimiser, which is a start as good as any.
+  bool exact = false;
+  if constexpr (NC && AK_NC_PREDICT) {
+    float ap[NV];
 #pragma unroll
-  for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
+    for (int i = 0; i < NV; i++) ap[i] = sv.a0[i];
+    {  // minimal diagonal-mass-norm move of the two steer accelerations onto J_eq a = 0
+      const float m1 = sv.M[EQ_DOF1][EQ_DOF1], m2 = sv.M[EQ_DOF2][EQ_DOF2];
+      const float je = ap[EQ_DOF1] + eqc2 * ap[EQ_DOF2];
+      const float lam = je * frcp(1.0f / m1 + eqc2 * eqc2 / m2);
+      ap[EQ_DOF1] -= lam / m1;
+      ap[EQ_DOF2] -= lam * eqc2 / m2;
+    }
+    int pst[NSCAL];  // predicted state: friction loss -1 / 0 (quadratic) / +1, limit 1 = active
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      const float xp = scal_J_dot(r, ap) - sj[r];
+      if (r == 0) pst[r] = 0;
+      else if (r <= 6) {
+        const float x = fabsf(xp) > 50.0f * sRfl[r] ? xp : scal_J_dot(r, warm_u) - sj[r];
+        pst[r] = x <= -sRfl[r] ? -1 : (x >= sRfl[r] ? 1 : 0);
+      } else pst[r] = xp < 0.0f ? 1 : 0;
+    }
+    // one Newton step from qacc_smooth on the predicted piece (gradient of that piece at a0)
+#pragma unroll
+    for (int i = 0; i < NV; i++) a[i] = sv.a0[i];
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
+    float H[NV][NV], grad[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+      grad[i] = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NV; j++) H[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      if (!sact[r]) continue;
+      int d1, d2;
+      float c1;
+      scal_dofs(r, d1, c1, d2);
+      const bool quad = (r == 0) || (r <= 6 ? pst[r] == 0 : pst[r] == 1);
+      const float f = quad ? -sD[r] * sj[r] : (r <= 6 ? -(float)pst[r] * sfl[r] : 0.0f);
+      grad[d1] -= f * c1;
+      if (d2 >= 0) grad[d2] -= f * eqc2;
+      if (quad) {
+        H[d1][d1] += sD[r] * c1 * c1;
+        if (d2 >= 0) {
+          H[d2][d2] += sD[r] * eqc2 * eqc2;
+          if (d2 > d1) H[d2][d1] += sD[r] * c1 * eqc2;
+          else H[d1][d2] += sD[r] * c1 * eqc2;
+        }
+      }
+    }
+    chol_sp<LANE_K(1)>(H);
+    float pdir[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
+    chol_sp_solve<LANE_K(1)>(H, pdir);
+#pragma unroll
+    for (int i = 0; i < NV; i++) a[i] += pdir[i];
+    int changed = 0;
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) {
+      const float x = sj[r] + scal_J_dot(r, pdir);
+      sj[r] = x;
+      if (sact[r] && r > 0) {
+        const int s1 = r <= 6 ? (x <= -sRfl[r] ? -1 : (x >= sRfl[r] ? 1 : 0)) : (x < 0.0f ? 1 : 0);
+        changed += s1 != pst[r];
+      }
+    }
+    exact = changed == 0;
+  } else {
+    // scalar jar at a
+#pragma unroll
+    for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
+  }
 
   STAMP(5);
   // ---------------- Newton iterations
@@ -1268,7 +1354,6 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   // state -- within a fixed active set the cost is quadratic, so that step was exact -- or when
   // the gradient is at the f32 noise floor of its two cancelling parts (rows flickering at a
   // region boundary), or after MAXIT iterations.
-  bool exact = false;
   int it_done = MAXIT, why = 4;
   NT_DECL
   NT_START;
