@@ -42,6 +42,12 @@ PPO_SOURCES = source_closure(os.path.join(CSRC, "ackppo.hip"))
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-fast-math",
                "-Wno-unused-result"]
+# Step kernels: no SLP vectorisation. At -O3 the compiler packs adjacent scalar f32 ops into
+# v_pk_*_f32, which needs operand pairs in consecutive registers: in these register-bound,
+# one-wave-per-SIMD kernels that cost more in moves and AGPR spills than it saved (nc kernel:
+# 10.9k -> 9.4k static instructions, 1109 -> 357 v_mov; measured 14.78 -> 13.67 us per step,
+# contacts-on quad 75.4 -> 70.1 us, obstacles 82.3 -> 76.6 us). The PPO kernels measured even.
+PHYS_FLAGS = ["-fno-slp-vectorize"]
 
 
 class ExtensionMissing(RuntimeError):
@@ -55,14 +61,14 @@ class EnvParams(C.Structure):
                 ("max_angular_velocity", C.c_double)]
 
 
-def _hipcc(out: str, sources: list, verbose: bool, force: bool) -> str:
+def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:
     if not force and os.path.exists(out):
         t = os.path.getmtime(out)
         if all(os.path.getmtime(s) <= t for s in sources):
             return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", out + ".tmp", sources[0]]
+    cmd = [hipcc, *HIPCC_FLAGS, *extra, "-o", out + ".tmp", sources[0]]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{r.stdout}\n{r.stderr}")
@@ -76,7 +82,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     """Compile the HIP sources for gfx950 into csrc/build/ (in-tree): libackphys.so (physics
     step, include/ackphys.h) and libackppo.so (PPO learner, include/ackppo.h)."""
     _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force)
-    return _hipcc(LIB_PATH, SOURCES, verbose, force)
+    return _hipcc(LIB_PATH, SOURCES, verbose, force, tuple(PHYS_FLAGS))
 
 
 EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",

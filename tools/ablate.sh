@@ -16,7 +16,7 @@ while [ $# -ge 2 ]; do
   rm -rf "$T/mujoco_playground_amd/csrc/build"
   cp -r "$ROOT/include" "$T/include"
   (cd "$T/mujoco_playground_amd/csrc" && sed -i -E "$expr" ackphys_step.hip ackphys_quad.inc &&
-   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -Wno-unused-result \
+   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -fno-slp-vectorize -Wno-unused-result \
      -o "$OUT/$name.so" ackphys_step.hip && rm -rf "$T") &
   pids+=($!)
 done

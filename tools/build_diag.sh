@@ -3,5 +3,5 @@
 set -e
 cd "$(dirname "$0")/../mujoco_playground_amd/csrc"
 mkdir -p build
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -DAK_STAMPS \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -fno-slp-vectorize -DAK_STAMPS \
   -o build/libackphys_stamps.so ackphys_step.hip

@@ -3,5 +3,5 @@
 set -e
 cd "$(dirname "$0")/../mujoco_playground_amd/csrc"
 mkdir -p build
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -DAK_TRACE \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-fast-math -fno-slp-vectorize -DAK_TRACE \
   -o build/libackphys_trace.so ackphys_step.hip
