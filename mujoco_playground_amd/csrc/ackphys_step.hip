@@ -1264,13 +1264,13 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   // Predicted active set (contacts-off kernel). Within a fixed set of row states the cost is
   // quadratic, so ONE Newton step from any point on that piece lands on its minimiser, and if the
   // rows there are in the assumed states that minimiser is the optimum (strict convexity). The
-  // states are predicted from two points: qacc_smooth moved onto the steering equality (the servo
-  // drives one steer, the equality the other), which decides the rows it puts far from their
-  // friction-loss kinks (the actuated wheels and steers: |x| > 50 R floss), and qacc_warmstart
-  // for the rest (the unactuated front spins, which sit in the quadratic zone step after step).
-  // The f64 probe (tools/probes/active_set_probe.py) finds the exact final states this way for
-  // 99.35 % of env-steps on the benchmark workload; a miss continues with Newton from the piece's
-  // minimiser, which is a start as good as any.
+  // states are predicted at qacc_smooth moved onto the steering equality (the servo drives one
+  // steer, the equality the other), each friction-loss row as its own one-dof problem: its
+  // saturated force floss moves x by floss * invweight, so the row ends in the quadratic zone iff
+  // |x_p| <= R floss + floss invweight. The f64 probe (tools/probes/active_set_probe.py) finds the
+  // exact final states this way for 99.84 % of env-steps on the benchmark workload (the misses:
+  // steer pairs the equality does not hold together); a miss continues with Newton from the
+  // piece's minimiser, which is a start as good as any.
   bool exact = false;
   if constexpr (NC && AK_NC_PREDICT) {
     float ap[NV];
@@ -1289,8 +1289,8 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
       const float xp = scal_J_dot(r, ap) - sj[r];
       if (r == 0) pst[r] = 0;
       else if (r <= 6) {
-        const float x = fabsf(xp) > 50.0f * sRfl[r] ? xp : scal_J_dot(r, warm_u) - sj[r];
-        pst[r] = x <= -sRfl[r] ? -1 : (x >= sRfl[r] ? 1 : 0);
+        const float thr = sRfl[r] + sfl[r] * DOF_INVW[5 + r];
+        pst[r] = xp < -thr ? -1 : (xp > thr ? 1 : 0);
       } else pst[r] = xp < 0.0f ? 1 : 0;
     }
     // one Newton step from qacc_smooth on the predicted piece (gradient of that piece at a0)

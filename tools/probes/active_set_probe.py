@@ -8,6 +8,8 @@ not) with the states predicted by
   prev   : the previous step's final states (rows matched by type and dof)
   prev2  : the final states two steps back (period-2 chatter of the steering servo)
   smooth : the rows at qacc_smooth
+  oned   : (the kernel's rule) each friction-loss row as a one-dof problem at qacc_smooth moved
+           onto the steering equality: quadratic zone iff |x| <= R floss + floss invweight
 If a prediction is right, one solve of that piece's quadratic is the exact optimum (convexity), so
 the hit rate bounds what a predicted-active-set start can save over Newton from a start point.
 
@@ -57,9 +59,8 @@ def main():
     o.reset(st, seed=3)
     rng = np.random.default_rng(0)
     fl_c = FLAG_CONTACTS if a.contacts else 0
-    hist = [dict() for _ in range(n)]  # per env: [final states of t-1, of t-2] as {key: state}
     prevs = [[None, None] for _ in range(n)]
-    hits = {k: 0 for k in ("warm", "prev", "prev2", "smooth", "prev|prev2", "warm|prev2")}
+    hits = {k: 0 for k in ("warm", "prev", "prev2", "smooth", "prev|prev2", "warm|prev2", "oned")}
     total = 0
     wave = {k: [] for k in hits}
     for k in range(a.steps):
@@ -91,6 +92,14 @@ def main():
                 ok["prev2"][e] = np.array_equal(p2, fin)
                 ok["prev|prev2"][e] = ok["prev"][e] or ok["prev2"][e]
                 ok["warm|prev2"][e] = ok["warm"][e] or ok["prev2"][e]
+                M = d["qM"]
+                ap = d["qacc_smooth"].copy()
+                ap[8] = ap[10] = (M[8, 8] * ap[8] + M[10, 10] * ap[10]) / (M[8, 8] + M[10, 10])
+                xp = J @ ap - aref
+                thr = R * fl + fl * efc[:, 5]
+                po = states(typ, R, fl, xp)
+                po = np.where(typ == 1, np.where(xp < -thr, -1, np.where(xp > thr, 1, 0)), po)
+                ok["oned"][e] = np.array_equal(po, fin)
             prevs[e] = [dict(zip(keys, fin.tolist())), prevs[e][0]]
         if k >= a.warm:
             total += n
