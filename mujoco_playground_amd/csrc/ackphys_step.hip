@@ -1390,6 +1390,10 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   int it_done = MAXIT, why = 4;
   NT_DECL
   NT_START;
+  // wave-uniform skip when every lane is already exact (the predicted piece): otherwise the
+  // loop's invariant set-up, which the compiler hoists ahead of the first exit test, still runs
+  if (__builtin_amdgcn_ballot_w64(!exact) == 0ull) { it_done = 0; why = 1; }
+  else
 #pragma unroll 1
   for (int it = 0; it < MAXIT; it++) {
     if (exact) { it_done = it; if (why != 2) why = 1; break; }
