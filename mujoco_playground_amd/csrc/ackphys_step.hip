@@ -356,7 +356,7 @@ struct SymPat { bool nz[NV][NV]; };
 #define AK_LANE_DENSE 0
 #endif
 #ifndef AK_QUAD_DENSE
-#define AK_QUAD_DENSE 1  // measured: dense 90.2 us vs structured 95.5 us per contacts-on step
+#define AK_QUAD_DENSE 0  // measured (no-SLP build): structured 69.3 us vs dense 70.0 us per contacts-on step, obstacles 73.9 vs 76.3
 #endif
 #define LANE_K(k) (AK_LANE_DENSE ? 3 : (k))
 #ifndef AK_QUAD_START

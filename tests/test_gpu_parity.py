@@ -306,6 +306,35 @@ def test_bad_acceleration_redo(blob, variant, contacts):
     teacher_forced(sim, o, acts[2:], 2, flags, seed)
 
 
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_contacts_off_random_states(blob, seed):
+    """The contacts-off kernel solves a predicted piece of the constraint problem first and falls
+    back to Newton when the rows end elsewhere; on the benchmark workload every lane is exact at
+    the prediction, so this test drives it from random states (tilted / airborne chassis, steers
+    beyond their limits, large wheel and steer speeds, arbitrary warmstarts) where predictions
+    miss, and holds every step to the oracle with the standard tolerances."""
+    n = 512
+    rng = np.random.default_rng(seed)
+    sim = make_sim(n, seed=seed, contacts=False, variant="lane")
+    sim.reset()
+    st = f64_state(sim.state)
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    st[:, 0:3] = rng.uniform(-2, 2, (n, 3))
+    st[:, 3:7] = q
+    st[:, 7:13] = rng.uniform(-3, 3, (n, 6))
+    st[:, [9, 11]] = rng.uniform(-0.8, 0.8, (n, 2))          # steers, limits at +-0.611
+    st[:, 13:19] = rng.normal(0, 2, (n, 6))                   # chassis twist
+    st[:, 19:25] = rng.normal(0, 20, (n, 6))                  # hinge speeds
+    st[:, [21, 23]] = rng.normal(0, 3, (n, 2))                # steer speeds
+    st[:, 25:37] = rng.normal(0, 50, (n, 12))                 # warmstarts
+    g = st.T.astype(np.float32)
+    g[42:44] = st[:, 42:44].T.astype(np.uint32).view(np.float32)
+    sim.set_state(torch.tensor(g, device=DEV))
+    acts = sim.random_actions(4, seed=seed)
+    teacher_forced(sim, fresh_oracle(blob), acts, 4, 2, seed)
+
+
 @pytest.mark.parametrize("variant", ["quad", "lane"])
 def test_sharding_is_exact(variant):
     """Two half-size shards with env offsets reproduce the unsharded run bit for bit."""
