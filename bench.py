@@ -50,7 +50,7 @@ def algorithmic_bytes_per_env_step() -> int:
 SETTLE_STEPS = 200
 
 
-def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat"):
+def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat", graph=False):
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
                               env_offset=shard.env_offset(rank, n_env), variant=variant, scene=scene)
     sim.reset()
@@ -59,6 +59,16 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     warmup = pre
     for k in range(warmup):
         sim.step(actions[k], want_info=False)
+    step_actions = actions[warmup:].unbind(0)  # per-step views, made before the timed region
+    g = None
+    if graph:  # the K timed steps as one captured hipGraph (same launches, same buffers)
+        snap = sim.state.clone(), sim.episode.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(steps):
+                sim.step(step_actions[k], want_info=False)
+        sim.state.copy_(snap[0])  # capture launches nothing, but restore anyway
+        sim.episode.copy_(snap[1])
     stream = torch.cuda.current_stream(device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
@@ -66,8 +76,11 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for k in range(steps):
-        sim.step(actions[warmup + k], want_info=False)
+    if g is not None:
+        g.replay()
+    else:
+        for k in range(steps):
+            sim.step(step_actions[k], want_info=False)
     ev1.record(stream)
     gathered = shard.gather_episode_stats(sim.episode, world)  # the per-rollout RCCL exchange
     torch.cuda.synchronize(device)
@@ -235,13 +248,14 @@ def main():
     ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane", "lane16"], help="step-kernel lane mapping")
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO-rollout leg (BASELINE configs[3])")
     ap.add_argument("--no-obstacles", action="store_true", help="skip the obstacle-scene leg (configs[4] world)")
+    ap.add_argument("--graph", action="store_true", help="replay the timed steps as one captured hipGraph")
     a = ap.parse_args()
     rank, world, local = shard.init()
     device = shard.device_for(local)
     torch.cuda.set_device(device)
     contacts = bool(a.contacts)
     sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
-                                             variant=a.variant)
+                                             variant=a.variant, graph=a.graph)
     total_envs = a.envs * world
     value = total_envs * a.steps / elapsed
     secondary = None

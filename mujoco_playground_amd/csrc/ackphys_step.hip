@@ -159,13 +159,27 @@ __device__ __forceinline__ void cross(float r[3], const float a[3], const float 
 __device__ __forceinline__ float dot(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }  // NaN or huge
 
-// Reciprocal / division / square-root helpers. Measured on MI355X (tools/variant_sweep.sh): the
-// hardware v_rcp/v_rsq/v_sqrt forms and a Cody-Waite/Cephes sincos cut instructions but made the
-// lane kernel's register allocation worse (36.7 -> 37.9 us/step contacts off), so the IEEE forms stay.
+// Reciprocal / division / square-root helpers (and the Cholesky pivots): the hardware 1-ulp
+// v_rcp / v_rsq / v_sqrt forms. With SLP vectorisation on they made the register allocation worse
+// (36.7 -> 37.9 us/step contacts off); in the no-SLP build they measure faster (nc kernel 9.05 ->
+// 8.75 us, contacts on 69.2 -> 68.7 us; tools/variant_sweep.sh) and every parity test holds.
+// AK_HWMATH=0 restores the correctly rounded forms.
+#ifndef AK_HWMATH
+#define AK_HWMATH 1
+#endif
+#if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt (variant builds only)
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+#define AK_PIVOT_RSQ(x) __builtin_amdgcn_rsqf(x)
+#else
 __device__ __forceinline__ float frcp(float x) { return 1.0f / x; }
 __device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
 __device__ __forceinline__ float frsq(float x) { return 1.0f / sqrtf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return sqrtf(x); }
+#define AK_PIVOT_RSQ(x) __frsqrt_rn(x)
+#endif
 __device__ __forceinline__ void fsincos(float x, float& s, float& c) { sincosf(x, &s, &c); }
 // wrap to [-pi, pi] (atan2(sin a, cos a) of the reference) for |a| <= 3 pi
 __device__ __forceinline__ float wrap_pi(float a) {
@@ -452,7 +466,7 @@ __device__ __forceinline__ void chol_sp(float H[NV][NV]) {
 #pragma unroll
     for (int k = 0; k < j; k++)
       if (LPAT[KIND].nz[j][k]) s -= AK_F(H, j, k) * AK_F(H, j, k);
-    const float inv = __frsqrt_rn(fmaxf(s, 1e-30f));
+    const float inv = AK_PIVOT_RSQ(fmaxf(s, 1e-30f));
     AK_F(H, j, j) = inv;
 #pragma unroll
     for (int i = j + 1; i < NV; i++) {

@@ -23,6 +23,16 @@ def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+def _raw_stream(device_index: int) -> int:
+    """hipStream_t of torch's current stream on the device (the stream every launch is enqueued on)."""
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
+if hasattr(torch._C, "_cuda_getCurrentRawStream"):  # same value, without building a Stream object
+    def _raw_stream(device_index: int) -> int:  # noqa: F811
+        return torch._C._cuda_getCurrentRawStream(device_index)
+
+
 class BatchedAckermannSim:
     def __init__(self, num_envs: int, device="cuda:0", seed: int = 0, contacts: bool = True,
                  env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
@@ -60,6 +70,11 @@ class BatchedAckermannSim:
         self.trunc = torch.zeros(self.n, dtype=u8, device=d)
         self.info = torch.zeros(4, self.n, dtype=f32, device=d)
         self.episode = torch.zeros(4, self.n, dtype=f32, device=d)
+        # the buffers are never reallocated (set_state copies in place): their C pointers are built
+        # once, so a step costs one ctypes call and a handful of attribute reads on the host
+        self._c = {k: C.c_void_p(getattr(self, k).data_ptr()) for k in
+                   ("state", "obs_soa", "terminal_obs_soa", "reward", "term", "trunc", "info", "episode")}
+        self._dev_index = self.device.index or 0
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
@@ -72,7 +87,7 @@ class BatchedAckermannSim:
         return (CONTACTS if self.contacts else 0) | (POSTSTEP_OBS if self.poststep_obs else 0)
 
     def _stream(self):
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return C.c_void_p(_raw_stream(self._dev_index))
 
     def reset(self, mask: torch.Tensor | None = None, seed: int | None = None) -> torch.Tensor:
         if seed is not None:
@@ -93,11 +108,13 @@ class BatchedAckermannSim:
         if actions.shape != (self.n, 2):
             raise ValueError(f"actions must be [{self.n}, 2], got {tuple(actions.shape)}")
         flags = self.flags | (AUTORESET if autoreset else 0)
-        _lib.check(_lib.lib().ackphys_step(
-            self._ctx, _ptr(actions), _ptr(self.state), _ptr(self.obs_soa), _ptr(self.reward), _ptr(self.term),
-            _ptr(self.trunc), _ptr(self.terminal_obs_soa) if (autoreset and want_terminal) else None,
-            _ptr(self.info) if want_info else None, _ptr(self.episode) if track_episodes else None, flags,
-            self.seed, self._stream()), "ackphys_step")
+        c = self._c
+        rc = _lib.lib().ackphys_step(
+            self._ctx, actions.data_ptr(), c["state"], c["obs_soa"], c["reward"], c["term"], c["trunc"],
+            c["terminal_obs_soa"] if (autoreset and want_terminal) else None, c["info"] if want_info else None,
+            c["episode"] if track_episodes else None, flags, self.seed, _raw_stream(self._dev_index))
+        if rc:
+            _lib.check(rc, "ackphys_step")
         return self.obs_soa, self.reward, self.term, self.trunc
 
     def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:

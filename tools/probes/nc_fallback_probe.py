@@ -38,6 +38,29 @@ def main():
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
     acts = torch.zeros(4, n, 2, device=dev)
+    # the benchmark workload's first steps from reset (the driver's short runs time steps 5..25)
+    n4 = 4096
+    ctx4 = P()
+    assert L.ackphys_create(blob, len(blob), n4, 0, C.byref(ctx4)) == 0
+    assert L.ackphys_set_variant(ctx4, 0) == 0
+    nb4 = (n4 + 63) // 64
+    st4 = torch.zeros(16 * nb4 + nb4 * 64 + 5 * nb4, dtype=torch.int64, device=dev)
+    state4, obs4 = torch.zeros(44, n4, device=dev), torch.zeros(79, n4, device=dev)
+    rew4, term4, trunc4 = (torch.zeros(n4, device=dev), torch.zeros(n4, dtype=torch.uint8, device=dev),
+                           torch.zeros(n4, dtype=torch.uint8, device=dev))
+    acts4 = torch.zeros(40, n4, 2, device=dev)
+    L.ackphys_random_actions(ctx4, p(acts4), 40, 0, 0, stream)
+    L.ackphys_reset(ctx4, None, 0, p(state4), p(obs4), stream)
+    assert L.ackphys_diag_set_stamps(p(st4)) == 0
+    for k in range(40):
+        st4.zero_()
+        L.ackphys_step(ctx4, p(acts4[k]), p(state4), p(obs4), p(rew4), p(term4), p(trunc4), None, None, None, 2, 0,
+                       stream)
+        torch.cuda.synchronize()
+        it = st4.cpu().numpy()[16 * nb4: 16 * nb4 + 64 * nb4] // 8
+        w = it.reshape(-1, 64).max(1)
+        print(f"bench step {k}: lane hist {np.bincount(it, minlength=4)[:6]} wave-max hist {np.bincount(w, minlength=4)[:6]}")
+    assert L.ackphys_diag_set_stamps(p(stamps)) == 0
     for seed in (31, 32, 33):
         rng = np.random.default_rng(seed)
         st = np.zeros((n, 44))
