@@ -278,21 +278,51 @@ __device__ __forceinline__ ObsOut observe_head(const float p[3], const float q[4
   return o;
 }
 
-// site origin (ox, oy, RAY_Z) / direction (dxb, dyb, 0) in the chassis frame -> world; mj_ray
-// plane test (ray_plane) against the finite floor rectangle
+// Every rangefinder site sits at RAY_R * (its direction) + RAY_Z e_z in the chassis frame (sites at
+// R_z(5i deg) (r, 0, 0), rays along the site x-axis: ackermann_robot_v2.xml:83-86), so a ray's world
+// origin is the pose constant (cx, cy, c0) plus RAY_R times its world direction: per ray, three
+// two-term dot products instead of six three-term ones.
+constexpr float RAY_R = RAY_ORG[0][0];
+constexpr bool rays_radial() {
+  for (int i = 0; i < 72; i++) {
+    const float ex = RAY_ORG[i][0] - RAY_R * RAY_DIR[i][0], ey = RAY_ORG[i][1] - RAY_R * RAY_DIR[i][1];
+    if (ex > 1e-8f || ex < -1e-8f || ey > 1e-8f || ey < -1e-8f) return false;
+  }
+  return RAY_DIR[0][0] == 1.0f && RAY_DIR[0][1] == 0.0f;
+}
+static_assert(rays_radial(), "rangefinder sites must lie on a circle around the z axis, rays pointing outwards");
+struct RayFrame {
+  float cx, cy, c0;  // world position of the ring centre at RAY_Z
+  float r0, r1, r3, r4, r6, r7;  // the chassis rotation's columns x, y
+};
+__device__ __forceinline__ RayFrame ray_frame(const float p[3], const float R[9]) {
+  return RayFrame{p[0] + R[2] * RAY_Z, p[1] + R[5] * RAY_Z, p[2] + R[8] * RAY_Z, R[0], R[1], R[3], R[4], R[6], R[7]};
+}
+// The same test from the site's chassis-frame origin (ox, oy, RAY_Z) with the full transforms: the
+// lane kernels' observation wave keeps this form (measured: the ring form below made the nc kernel
+// 8.72 -> 8.90 us although it removes ~700 instructions; the quad kernels gain 68.6 -> 68.1 us).
 __device__ __forceinline__ float ray_floor_c(const float p[3], const float R[9], float ox, float oy, float dxb,
                                              float dyb) {
-  float dz = R[6] * dxb + R[7] * dyb;
-  float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
-  // branchless: t from the hardware reciprocal (1 ulp; within the f32 tolerance of the obs parity)
+  const float dz = R[6] * dxb + R[7] * dyb;
+  const float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
   const float t = -oz * __builtin_amdgcn_rcpf(dz);
   const float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
   const float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
   const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
   return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
 }
-__device__ __forceinline__ float ray_floor(const float p[3], const float R[9], int i) {
-  return ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
+// chassis-frame direction (dxb, dyb, 0) -> mj_ray's plane test against the finite floor rectangle;
+// distance from the site (t), clamped to the cutoff, -1 for no hit
+__device__ __forceinline__ float ray_floor_f(const RayFrame& F, float dxb, float dyb) {
+  const float dz = F.r6 * dxb + F.r7 * dyb;
+  const float ux = F.r0 * dxb + F.r1 * dyb, uy = F.r3 * dxb + F.r4 * dyb;
+  const float oz = fmaf(RAY_R, dz, F.c0);
+  // branchless: t from the hardware reciprocal (1 ulp; within the f32 tolerance of the obs parity)
+  const float t = -oz * __builtin_amdgcn_rcpf(dz);
+  const float s = t + RAY_R;
+  const float hx = fmaf(s, ux, F.cx), hy = fmaf(s, uy, F.cy);
+  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
+  return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
 }
 
 // ------------------------------------------------------------------ impedance / reference
@@ -332,9 +362,12 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   // rays 10..71 are observed; obs[0:10] alias sensordata[76] = ray 71 (name-lookup aliasing,
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
+  const RayFrame F = ray_frame(p, R);
 #pragma unroll
   for (int i = 10; i < 72; i++) {
-    float v = ray_scene<SC>(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
+    float v;
+    if constexpr (SC == 0) v = ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
+    else v = ray_scene<SC>(F, RAY_DIR[i][0], RAY_DIR[i][1]);
     stf(dst, i, vo, v);
     minl = fminf(minl, v);
     v71 = v;
@@ -1785,9 +1818,17 @@ __device__ __forceinline__ void step_serial(const Args& A, float* lds, int lane,
 //   barrier 2: wave 1 -> wave 0 "auto-reset this env" (term from the goal distance, trunc), after
 //              wave 1 has written obs, so wave 0's reset observation lands last.
 // The observation leaves the critical path (~20 % of the serial step).
+// true if some env of the workgroup (npair dynamics waves x 64) was redone: the same answer in
+// every wave, so the conditional barrier 2 is workgroup-uniform
+__device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int npair) {
+  bool r = false;
+  for (int w = 0; w < npair; w++) r |= sh_bad[w * 64 + lane] != 0;
+  return r;
+}
+
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t* sh_bad, const uint8_t* sh_reset,
-                                              int lane, int e, bool valid) {
+                                              int lane, int e, bool valid, int slot, int npair) {
   const int n = A.n;
   Slots S{lds + lane};
   const uint32_t vo = 4u * (uint32_t)e;
@@ -1845,14 +1886,14 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
       break;
     }
   }
-  sh_bad[lane] = redo ? 1 : 0;
+  sh_bad[slot] = redo ? 1 : 0;
   __syncthreads();  // 1: wave 1 has written obs and the auto-reset decisions; it learns the redos
-  // 2 (only when some env of the workgroup was redone; both waves read the same 64 bytes): wave 1
+  // 2 (only when some env of the workgroup was redone; every wave reads the same bytes): wave 1
   // has re-observed the redone envs at qpos0 and revised their auto-reset decisions
-  if (__builtin_amdgcn_ballot_w64(sh_bad[lane] != 0) != 0ull) __syncthreads();
+  if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, npair)) != 0ull) __syncthreads();
   if (!valid) return;
   STAMP(9);
-  if (sh_reset[lane]) {
+  if (sh_reset[slot]) {
     reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm);
     return;
   }
@@ -1867,7 +1908,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
 }
 
 __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
-                                              bool valid) {
+                                              bool valid, int slot, int npair) {
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
   const Soa st = soa(A.state, NSTATE, n);
@@ -1924,11 +1965,11 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
     }
     // terminal obs before wave 0 may overwrite obs with the reset observation
     if (A.tobs) copy_terminal_obs(obs, soa(A.tobs, NOBS, n), vo, autoreset && (pass == 0 || redo));
-    sh_reset[lane] = autoreset ? 1 : 0;
+    sh_reset[slot] = autoreset ? 1 : 0;
     __syncthreads();  // pass 0: barrier 1; pass 1: barrier 2 (see step_dyn_wave)
     if (pass == 1) break;
-    if (__builtin_amdgcn_ballot_w64(sh_bad[lane] != 0) == 0ull) break;
-    redo = valid && sh_bad[lane];
+    if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, npair)) == 0ull) break;
+    redo = valid && sh_bad[slot];
   }
   if (valid && A.ep) {
     // Monitor-wrapper episode bookkeeping (train.py:70): r/l of finished episodes
@@ -1953,20 +1994,28 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
   step_serial(A, lds, lane, e);
 }
 
-template <int NC>
+// PW wave pairs per workgroup: waves 0..PW-1 run the dynamics of envs [64 w, 64 w + 64) of the
+// block, waves PW..2PW-1 their observations (2 PW waves on the CU's 4 SIMDs)
+template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ uint8_t sh_bad[64], sh_reset[64];
+  __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * A.epw + lane;
+  const int pair = wave % PW, slot = pair * 64 + lane;
+  const int e = blockIdx.x * (A.epw * PW) + pair * A.epw + lane;
   const bool valid = lane < A.epw && e < A.n;
-  if (wave == 0) step_dyn_wave<NC>(A, lds, sh_bad, sh_reset, lane, e, valid);
-  else step_obs_wave(A, sh_bad, sh_reset, lane, e, valid);
+  if (wave < PW) step_dyn_wave<NC>(A, lds, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  else step_obs_wave(A, sh_bad, sh_reset, lane, e, valid, slot, PW);
 }
-extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) { step_split<0>(A); }
+#ifndef AK_NC_PW
+#define AK_NC_PW 1  // wave pairs per workgroup of the contacts-off kernel
+#endif
+extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) { step_split<0, 1>(A); }
 // contacts off (BASELINE configs[1]): the contact machinery is compiled out
-extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_nc_kernel(Args A) { step_split<1>(A); }
+extern "C" __global__ void __launch_bounds__(128 * AK_NC_PW, 1) ackphys_step_nc_kernel(Args A) {
+  step_split<1, AK_NC_PW>(A);
+}
 
 template <int SC>
 __device__ __forceinline__ void reset_body(const uint8_t* mask, float* state, float* obs, int n, uint64_t seed,
@@ -2153,13 +2202,14 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
       hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   } else {
     a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
-    int blocks = (ctx->n_env + a.epw - 1) / a.epw;
+    const int pw = (flags & (ACKPHYS_POSTSTEP_OBS | ACKPHYS_CONTACTS)) ? 1 : AK_NC_PW;
+    int blocks = (ctx->n_env + a.epw * pw - 1) / (a.epw * pw);
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else if (flags & ACKPHYS_CONTACTS)
       hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(128 * pw), 0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");
