@@ -4,18 +4,21 @@ Runs the f64 oracle on the benchmark workload (uniform random actions from reset
 env-step after a warm-up, compares the row states at the oracle's optimum (equality: always
 quadratic; friction loss: lower-linear / quadratic / upper-linear; limits and contacts: active or
 not) with the states predicted by
-  warm   : the rows at qacc_warmstart with this step's aref (= the current Newton's first iteration)
-  prev   : the previous step's final states (rows matched by type and dof)
-  prev2  : the final states two steps back (period-2 chatter of the steering servo)
+  warm   : the rows at qacc_warmstart with this step's aref (= the Newton's first iteration from it)
   smooth : the rows at qacc_smooth
-  oned   : (the kernel's rule) each friction-loss row as a one-dof problem at qacc_smooth moved
-           onto the steering equality: quadratic zone iff |x| <= R floss + floss invweight
-If a prediction is right, one solve of that piece's quadratic is the exact optimum (convexity), so
-the hit rate bounds what a predicted-active-set start can save over Newton from a start point.
+  oned   : each friction-loss row as a one-dof problem at qacc_smooth moved onto the steering
+           equality: quadratic zone iff |x| <= R floss + floss invweight
+  kernel : oned, with the two steer rows from the exact two-dof sub-problem (diagonal masses,
+           equality row, both Huber rows) -- the contacts-off kernel's rule
+and, with --contacts 1, "kernel+contacts": the kernel rule for the scalar rows plus pyramid-edge
+states from the steer-projected qacc_smooth ("kernel" then scores the scalar rows alone). The
+contact kernels do not use a prediction: too few hits.
+If a prediction is right, one solve of that piece's quadratic is the exact optimum (convexity).
 
-    python tools/probes/active_set_probe.py [--envs 256] [--steps 300] [--contacts 0]
+    python tools/probes/active_set_probe.py [--envs 256] [--steps 200] [--warm 60] [--contacts 0]
 """
 import argparse
+import itertools
 import os
 import sys
 
@@ -27,14 +30,7 @@ from mujoco_playground_amd import _lib  # noqa: E402
 from oracle.oracle import FLAG_AUTORESET, FLAG_CONTACTS, Oracle, controller  # noqa: E402
 
 FRICTIONLOSS = np.array([0, 0, 0, 0, 0, 0, 0.02, 0.02, 0.005, 0.012, 0.005, 0.012])
-
-
-def row_keys(typ, J):
-    keys = []
-    for t, j in zip(typ, J):
-        d = int(np.argmax(np.abs(j)))
-        keys.append((int(t), d if t in (1, 2) else -1, int(np.sign(j[d])) if t == 2 else 0))
-    return keys
+STEER = (8, 10)  # the equality's dofs (fl_steer = fr_steer)
 
 
 def states(typ, R, fl, x):
@@ -46,11 +42,32 @@ def states(typ, R, fl, x):
     return s
 
 
+def pair_states(M, a0, D, R, fl, aref, J, typ, i1, i2, ie, guess):
+    """exact states of the steer pair's two-dof sub-problem; the one-dof guess first"""
+    c = J[ie, STEER[1]] / J[ie, STEER[0]]
+    m1, m2 = M[STEER[0], STEER[0]], M[STEER[1], STEER[1]]
+    ae = aref[ie] / J[ie, STEER[0]]
+    for s1, s2 in [guess] + list(itertools.product((-1, 0, 1), repeat=2)):
+        H = np.diag([m1, m2]) + D[ie] * np.outer([1, c], [1, c])
+        b = np.array([m1 * a0[STEER[0]], m2 * a0[STEER[1]]]) + D[ie] * ae * np.array([1, c])
+        for k, (s, i) in enumerate(((s1, i1), (s2, i2))):
+            if s == 0:
+                H[k, k] += D[i]
+                b[k] += D[i] * aref[i]
+            else:
+                b[k] -= s * fl[i]
+        a = np.linalg.solve(H, b)
+        t = states(typ[[i1, i2]], R[[i1, i2]], fl[[i1, i2]], a - aref[[i1, i2]])
+        if (t[0], t[1]) == (s1, s2):
+            return s1, s2
+    return guess
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=256)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warm", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warm", type=int, default=60)
     ap.add_argument("--contacts", type=int, default=0)
     a = ap.parse_args()
     o = Oracle(_lib.load_blob())
@@ -59,57 +76,50 @@ def main():
     o.reset(st, seed=3)
     rng = np.random.default_rng(0)
     fl_c = FLAG_CONTACTS if a.contacts else 0
-    prevs = [[None, None] for _ in range(n)]
-    hits = {k: 0 for k in ("warm", "prev", "prev2", "smooth", "prev|prev2", "warm|prev2", "oned")}
+    names = ("warm", "smooth", "oned", "kernel") + (("kernel+contacts",) if a.contacts else ())
+    hits = {k: 0 for k in names}
     total = 0
-    wave = {k: [] for k in hits}
     for k in range(a.steps):
         act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
-        if k >= a.warm:
-            ok = {kk: np.zeros(n, bool) for kk in hits}
         for e in range(n):
+            if k < a.warm:
+                continue
             d = o.diag(st[e], controller(act[e]), flags=fl_c)
+            total += 1
             if d["nefc"] == 0:
-                prevs[e] = [{}, prevs[e][0]]
-                if k >= a.warm:
-                    for kk in hits:
-                        ok[kk][e] = True
+                for kk in names:
+                    hits[kk] += 1
                 continue
             efc, J = d["efc"], d["efc_J"]
             typ = efc[:, 0].astype(int)
-            R, aref = efc[:, 2], efc[:, 3]
-            fl = np.array([FRICTIONLOSS[np.argmax(np.abs(j))] if t == 1 else 0.0 for t, j in zip(typ, J)])
-            keys = row_keys(typ, J)
+            R, aref, invw = efc[:, 2], efc[:, 3], efc[:, 5]
+            D = 1.0 / R
+            dofs = np.array([int(np.argmax(np.abs(j))) for j in J])
+            fl = np.where(typ == 1, FRICTIONLOSS[dofs], 0.0)
+            M, a0 = d["qM"], d["qacc_smooth"]
             fin = states(typ, R, fl, J @ d["qacc"] - aref)
-            if k >= a.warm and a.contacts == 0:
-                pw = states(typ, R, fl, J @ st[e, 25:37] - aref)
-                ps = states(typ, R, fl, J @ d["qacc_smooth"] - aref)
-                p1 = np.array([prevs[e][0].get(kk, -9) if prevs[e][0] is not None else -9 for kk in keys])
-                p2 = np.array([prevs[e][1].get(kk, -9) if prevs[e][1] is not None else -9 for kk in keys])
-                ok["warm"][e] = np.array_equal(pw, fin)
-                ok["smooth"][e] = np.array_equal(ps, fin)
-                ok["prev"][e] = np.array_equal(p1, fin)
-                ok["prev2"][e] = np.array_equal(p2, fin)
-                ok["prev|prev2"][e] = ok["prev"][e] or ok["prev2"][e]
-                ok["warm|prev2"][e] = ok["warm"][e] or ok["prev2"][e]
-                M = d["qM"]
-                ap = d["qacc_smooth"].copy()
-                ap[8] = ap[10] = (M[8, 8] * ap[8] + M[10, 10] * ap[10]) / (M[8, 8] + M[10, 10])
-                xp = J @ ap - aref
-                thr = R * fl + fl * efc[:, 5]
-                po = states(typ, R, fl, xp)
-                po = np.where(typ == 1, np.where(xp < -thr, -1, np.where(xp > thr, 1, 0)), po)
-                ok["oned"][e] = np.array_equal(po, fin)
-            prevs[e] = [dict(zip(keys, fin.tolist())), prevs[e][0]]
-        if k >= a.warm:
-            total += n
-            for kk in hits:
-                hits[kk] += int(ok[kk].sum())
-                wave[kk].append(ok[kk].reshape(-1, 64).all(1).mean())
+            pred = {"warm": states(typ, R, fl, J @ st[e, 25:37] - aref), "smooth": states(typ, R, fl, J @ a0 - aref)}
+            ap_ = a0.copy()
+            w1, w2 = M[STEER[0], STEER[0]], M[STEER[1], STEER[1]]
+            ap_[STEER[0]] = ap_[STEER[1]] = (w1 * a0[STEER[0]] + w2 * a0[STEER[1]]) / (w1 + w2)
+            xp = J @ ap_ - aref
+            thr = R * fl + fl * invw
+            oned = np.where(typ == 1, np.where(xp < -thr, -1, np.where(xp > thr, 1, 0)), states(typ, R, fl, xp))
+            pred["oned"] = oned
+            kern = oned.copy()
+            i1 = np.nonzero((typ == 1) & (dofs == STEER[0]))[0][0]
+            i2 = np.nonzero((typ == 1) & (dofs == STEER[1]))[0][0]
+            ie = np.nonzero(typ == 0)[0][0]
+            kern[i1], kern[i2] = pair_states(M, a0, D, R, fl, aref, J, typ, i1, i2, ie, (oned[i1], oned[i2]))
+            pred["kernel"] = kern
+            if a.contacts:
+                pred["kernel+contacts"] = np.where(typ >= 3, states(typ, R, fl, xp), kern)
+                pred["kernel"] = np.where(typ >= 3, fin, kern)  # scalar rows only
+            for kk in names:
+                hits[kk] += int(np.array_equal(pred[kk], fin))
         o.step(st, act, flags=fl_c | FLAG_AUTORESET, seed=3)
-    for kk in hits:
-        print(f"{kk:11s} env-step hit rate {hits[kk] / max(total, 1):.4f}   all-64-lanes-hit rate "
-              f"{np.mean(wave[kk]) if wave[kk] else 0:.4f}")
+    for kk in names:
+        print(f"{kk:16s} env-step hit rate {hits[kk] / max(total, 1):.5f}  ({total} env-steps)")
 
 
 if __name__ == "__main__":
