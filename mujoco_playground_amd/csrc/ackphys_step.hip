@@ -167,7 +167,7 @@ __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }
 #ifndef AK_HWMATH
 #define AK_HWMATH 1
 #endif
-#if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt (variant builds only)
+#if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -202,6 +202,7 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // ------------------------------------------------------------------ controller (f64)
 // BicycleController.cmd_vel_to_controls + apply_cmd_vel, controller.py:98-140, evaluated in
 // float64 exactly like the reference (its thresholds 1e-6 / 1e-5 sit on f64 values).
+template <bool BF = false>  // BF: branch-free form (same values), chosen per kernel by measurement
 __device__ __forceinline__ void controller(float a0f, float a1f, float max_lin, float max_ang, float ctrl[3], bool& bad) {
   // np.clip on the float32 action, then action * max_velocity: float32 x Python float stays
   // float32 under NumPy 2 promotion (ackermann_env.py:190-194); controller works in float64.
@@ -214,17 +215,30 @@ __device__ __forceinline__ void controller(float a0f, float a1f, float max_lin, 
   const double L = 0.20, T = 0.174, rw = 0.0325, eps = 1e-5;
   const double TAN_LIM = 0.70020753820970977;  // tan(35 deg) (controller.py:112)
   const double v = (double)(a0f * max_lin), om = (double)(a1f * max_ang);
-  double y = 0.0;
-  if (!(fabs(om) < 1e-6)) {
+  double y = 0.0, vl = v, vr = v;
+  if constexpr (BF) {
+    // both sides evaluated and selected (no basic-block boundaries, so the scheduler can interleave
+    // the f64 chain with the kinematics); a zero denominator only arises when om == 0, whose y is 0.
+    // Measured: contacts-on quad kernel 68.2 -> 66.5 us; the obstacle kernel 73.8 -> 74.9 us and
+    // the lane kernels even, so only the flat-scene quad kernel uses it.
     const double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
-    y = (L * om) / den;
-  }
-  double vl = v, vr = v;
-  if (!(fabs(y) < 1e-6)) {
+    y = fabs(om) < 1e-6 ? 0.0 : (L * om) / den;
     const double t = fabs(y) > TAN_LIM ? copysign(TAN_LIM, y) : y;
     const double k = fabs(t) > eps ? t * (T / (2.0 * L)) : __builtin_nan("");
-    vl = v * (1.0 - k);
-    vr = v * (1.0 + k);
+    const bool straight = fabs(y) < 1e-6;
+    vl = straight ? v : v * (1.0 - k);
+    vr = straight ? v : v * (1.0 + k);
+  } else {
+    if (!(fabs(om) < 1e-6)) {
+      const double den = fabs(v) > eps ? v : (double)((om > 0) - (om < 0)) * eps;
+      y = (L * om) / den;
+    }
+    if (!(fabs(y) < 1e-6)) {
+      const double t = fabs(y) > TAN_LIM ? copysign(TAN_LIM, y) : y;
+      const double k = fabs(t) > eps ? t * (T / (2.0 * L)) : __builtin_nan("");
+      vl = v * (1.0 - k);
+      vr = v * (1.0 + k);
+    }
   }
   const double wl = vl * (1.0 / rw), wr = vr * (1.0 / rw);
   const float c0 = fminf(fmaxf(atanf((float)y), -0.61f), 0.61f);  // clip(delta, +-0.61)
