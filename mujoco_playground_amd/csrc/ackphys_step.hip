@@ -1112,6 +1112,28 @@ __device__ __forceinline__ void euler_advance(const float u[NV], const StepResul
   for (int i = 3; i < NV; i++) warm[i] = res.qacc[i];
 }
 
+// chassis-frame velocities / warmstart (u coordinates) of the loaded state
+__device__ __forceinline__ void to_u(const float qpos[13], const float qvel[NV], const float warm[NV], float R[9],
+                                     float u[NV], float wu[NV]) {
+  float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
+  normq(q);
+  quat_R(q, R);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    u[k] = R[k] * qvel[0] + R[3 + k] * qvel[1] + R[6 + k] * qvel[2];
+    wu[k] = R[k] * warm[0] + R[3 + k] * warm[1] + R[6 + k] * warm[2];
+  }
+#pragma unroll
+  for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
+}
+__device__ __forceinline__ void reset_to_qpos0(float qpos[13], float qvel[NV], float warm[NV], float ctrl[3]) {
+#pragma unroll
+  for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
+  ctrl[0] = ctrl[1] = ctrl[2] = 0.0f;
+}
+
 // Pose the observation is taken at. Default: the pre-integration pose (mj_step's sensors and x*
 // arrays). F_POSTSTEP_OBS: render_mode="human" (ackermann_env.py:202-207) runs mj_forward after
 // mj_step, so obs/reward see the integrated pose.
@@ -1126,29 +1148,133 @@ __device__ __forceinline__ void obs_pose(uint32_t flags, const float qpos[13], f
   }
 }
 
-// forward dynamics + constraint solve for one env (state in registers), u coordinates
-template <int NC>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
-__device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
-                         const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
-  // front steer angles -> spin / cylinder axes in the chassis frame
+// Scalar constraint rows (equality, dof friction loss, joint limits) of one env: their reference
+// accelerations aref (jar = J a - aref), D = 1/R, the Huber width R floss and floss, and which
+// rows exist. They read only hinge positions and hinge speeds (u = qvel there), so the lane
+// kernels' observation wave computes them beside the dynamics wave (see step_split).
+struct ScalRows {
+  float aref[NSCAL], D[NSCAL], Rfl[NSCAL], fl[NSCAL];
+  bool act[NSCAL];
+  float eqc2;  // equality row J = e_EQ_DOF1 + eqc2 e_EQ_DOF2
+};
+static_assert(EQ_DOF1 >= 6 && EQ_DOF2 >= 6, "equality between hinge dofs");
+__device__ __forceinline__ void scalar_rows(const float qpos[13], const float u[NV], ScalRows& r_) {
+  float K, B;
+  ref_kb(K, B);
+  {
+    // equality (polycoef), pos and diagApprox
+    const float dif = qpos[EQ_QPOS2] - QPOS0[EQ_QPOS2];
+    const float cpos = EQ_POLY[0] + dif * (EQ_POLY[1] + dif * (EQ_POLY[2] + dif * (EQ_POLY[3] + dif * EQ_POLY[4])));
+    const float cvel = EQ_POLY[1] + dif * (2 * EQ_POLY[2] + dif * (3 * EQ_POLY[3] + dif * 4 * EQ_POLY[4]));
+    r_.eqc2 = -cvel;
+    const float pos = qpos[EQ_QPOS1] - QPOS0[EQ_QPOS1] - cpos;
+    const float imp = impedance(pos);
+    const float diag = DOF_INVW[EQ_DOF1] + DOF_INVW[EQ_DOF2];
+    const float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * diag);
+    r_.D[0] = frcp(Rr); r_.Rfl[0] = 0; r_.fl[0] = 0; r_.act[0] = true;
+    const float jv = u[EQ_DOF1] + r_.eqc2 * u[EQ_DOF2];
+    r_.aref[0] = -B * jv - K * imp * pos;
+  }
+#pragma unroll
+  for (int r = 1; r <= 6; r++) {
+    const int d = 5 + r;
+    const float imp = impedance(0.0f);
+    const float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[d]);
+    r_.D[r] = frcp(Rr); r_.fl[r] = FRICTIONLOSS[d]; r_.Rfl[r] = Rr * FRICTIONLOSS[d];
+    r_.act[r] = FRICTIONLOSS[d] > 0.0f;
+    r_.aref[r] = -B * u[d];
+  }
+#pragma unroll
+  for (int r = 7; r < NSCAL; r++) {
+    const int l = (r - 7) >> 1, side = ((r - 7) & 1) ? 1 : -1;
+    const float q = qpos[LIM_QPOS[l]];
+    const float dist = side * (LIM_RANGE[l][side > 0 ? 1 : 0] - q);
+    r_.act[r] = dist < 0.0f;
+    const float imp = impedance(dist);
+    const float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[LIM_DOF[l]]);
+    r_.D[r] = frcp(Rr); r_.fl[r] = 0; r_.Rfl[r] = 0;
+    const float jv = -side * u[LIM_DOF[l]];
+    r_.aref[r] = -B * jv - K * imp * dist;
+  }
+}
+// the state-dependent words of ScalRows through LDS ([word][slot], conflict-free): aref 0..10,
+// D of the equality and the limits, the limits' existence bits, eqc2; the rest is constant
+constexpr int XCH_ROWS = NSCAL + 1 + (NSCAL - 7) + 1 + 1;  // + ctrl 3
+constexpr int XCH_WORDS = XCH_ROWS + 3;
+__device__ __forceinline__ void xch_put(float* x, int slot, int stride, const ScalRows& r, const float ctrl[3]) {
+  int w = 0;
+#pragma unroll
+  for (int k = 0; k < NSCAL; k++) x[(w++) * stride + slot] = r.aref[k];
+  x[(w++) * stride + slot] = r.D[0];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 7; k < NSCAL; k++) {
+    x[(w++) * stride + slot] = r.D[k];
+    bits |= (r.act[k] ? 1u : 0u) << k;
+  }
+  x[(w++) * stride + slot] = __uint_as_float(bits);
+  x[(w++) * stride + slot] = r.eqc2;
+#pragma unroll
+  for (int k = 0; k < 3; k++) x[(w++) * stride + slot] = ctrl[k];
+}
+__device__ __forceinline__ void xch_get(const float* x, int slot, int stride, ScalRows& r, float ctrl[3]) {
+  int w = 0;
+#pragma unroll
+  for (int k = 0; k < NSCAL; k++) r.aref[k] = x[(w++) * stride + slot];
+  r.D[0] = x[(w++) * stride + slot];
+  r.Rfl[0] = 0; r.fl[0] = 0; r.act[0] = true;
+#pragma unroll
+  for (int k = 1; k <= 6; k++) {  // friction loss: constants (impedance at pos 0)
+    const int d = 5 + k;
+    const float imp = impedance(0.0f);
+    const float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[d]);
+    r.D[k] = frcp(Rr); r.fl[k] = FRICTIONLOSS[d]; r.Rfl[k] = Rr * FRICTIONLOSS[d];
+    r.act[k] = FRICTIONLOSS[d] > 0.0f;
+  }
+#pragma unroll
+  for (int k = 7; k < NSCAL; k++) { r.D[k] = x[(w++) * stride + slot]; r.fl[k] = 0; r.Rfl[k] = 0; }
+  const uint32_t bits = __float_as_uint(x[(w++) * stride + slot]);
+#pragma unroll
+  for (int k = 7; k < NSCAL; k++) r.act[k] = (bits >> k) & 1u;
+  r.eqc2 = x[(w++) * stride + slot];
+#pragma unroll
+  for (int k = 0; k < 3; k++) ctrl[k] = x[(w++) * stride + slot];
+}
+
+// forward dynamics, first part (no control): steer-dependent axes, mass matrix, bias, passive
+struct DynPre {
   float sa[2][3], cyl[2][3];
+  Solver sv;  // M; fs = -bias - damping (actuator forces added in dyn_post)
+};
+__device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV], const float R[9], DynPre& P) {
+  // front steer angles -> spin / cylinder axes in the chassis frame
 #pragma unroll
   for (int s = 0; s < 2; s++) {
     float d = qpos[W_STEER_QPOS[2 + s]];
     float c, sn;
     fsincos(d, sn, c);
-    rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
-    rot_axis(cyl[s], S_AXIS[s], W_CYL_AXIS[2 + s], c, sn);
+    rot_axis(P.sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
+    rot_axis(P.cyl[s], S_AXIS[s], W_CYL_AXIS[2 + s], c, sn);
   }
   STAMP(2);
-  Solver sv;
-  build_M(sv.M, sa);
+  build_M(P.sv.M, P.sa);
   float b[NV];
-  bias(u, R, sa, b);
-  // passive damping + actuators (mj_passive, mj_fwdActuation)
+  bias(u, R, P.sa, b);
+  // passive damping (mj_passive)
 #pragma unroll
-  for (int i = 0; i < NV; i++) sv.fs[i] = -b[i] - DAMPING[i] * u[i];
-  {
+  for (int i = 0; i < NV; i++) P.sv.fs[i] = -b[i] - DAMPING[i] * u[i];
+}
+
+// forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
+template <int NC>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
+__device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
+                                         const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
+                                         const ScalRows& sr, StepResult& out) {
+  float(&sa)[2][3] = P.sa;
+  float(&cyl)[2][3] = P.cyl;
+  Solver& sv = P.sv;
+  (void)sa;
+  {  // actuators (mj_fwdActuation)
     float c0 = ctrl[0];
     if (ACT_CTRLLIMITED[0]) c0 = fminf(fmaxf(c0, ACT_CTRLRANGE[0][0]), ACT_CTRLRANGE[0][1]);
     float f0 = ACT_GAIN[0] * c0 + ACT_BIAS1[0] * qpos[ACT_STEER_QPOS] + ACT_BIAS2[0] * u[ACT_STEER_DOF];
@@ -1205,43 +1331,14 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   // scalar rows: jar, D, type, R*floss
   float sj[NSCAL], sD[NSCAL], sRfl[NSCAL], sfl[NSCAL], sjp[NSCAL];
   bool sact[NSCAL];
-  float eqc2;
-  {
-    // equality (polycoef), pos and diagApprox
-    float dif = qpos[EQ_QPOS2] - QPOS0[EQ_QPOS2];
-    float cpos = EQ_POLY[0] + dif * (EQ_POLY[1] + dif * (EQ_POLY[2] + dif * (EQ_POLY[3] + dif * EQ_POLY[4])));
-    float cvel = EQ_POLY[1] + dif * (2 * EQ_POLY[2] + dif * (3 * EQ_POLY[3] + dif * 4 * EQ_POLY[4]));
-    eqc2 = -cvel;
-    float pos = qpos[EQ_QPOS1] - QPOS0[EQ_QPOS1] - cpos;
-    float imp = impedance(pos);
-    float diag = DOF_INVW[EQ_DOF1] + DOF_INVW[EQ_DOF2];
-    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * diag);
-    sD[0] = frcp(Rr); sRfl[0] = 0; sfl[0] = 0; sact[0] = true;
-    float ja = warm_u[EQ_DOF1] + eqc2 * warm_u[EQ_DOF2];
-    float jv = u[EQ_DOF1] + eqc2 * u[EQ_DOF2];
-    sj[0] = -B * jv - K * imp * pos;  // holds aref for now
-    (void)ja;
-  }
+  const float eqc2 = sr.eqc2;
 #pragma unroll
-  for (int r = 1; r <= 6; r++) {
-    int d = 5 + r;
-    float imp = impedance(0.0f);
-    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[d]);
-    sD[r] = frcp(Rr); sfl[r] = FRICTIONLOSS[d]; sRfl[r] = Rr * FRICTIONLOSS[d];
-    sact[r] = FRICTIONLOSS[d] > 0.0f;
-    sj[r] = -B * u[d];
-  }
-#pragma unroll
-  for (int r = 7; r < NSCAL; r++) {
-    int l = (r - 7) >> 1, side = ((r - 7) & 1) ? 1 : -1;
-    float q = qpos[LIM_QPOS[l]];
-    float dist = side * (LIM_RANGE[l][side > 0 ? 1 : 0] - q);
-    sact[r] = dist < 0.0f;
-    float imp = impedance(dist);
-    float Rr = fmaxf(MINVAL, fdiv(1 - imp, imp) * DOF_INVW[LIM_DOF[l]]);
-    sD[r] = frcp(Rr); sfl[r] = 0; sRfl[r] = 0;
-    float jv = -side * u[LIM_DOF[l]];
-    sj[r] = -B * jv - K * imp * dist;
+  for (int r = 0; r < NSCAL; r++) {
+    sj[r] = sr.aref[r];  // holds aref for now
+    sD[r] = sr.D[r];
+    sRfl[r] = sr.Rfl[r];
+    sfl[r] = sr.fl[r];
+    sact[r] = sr.act[r];
   }
   // aref of scalar rows is in sj; jar(a) = J a - aref
 
@@ -1647,6 +1744,17 @@ __device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const f
   STAMP(7);
 }
 
+// forward dynamics + constraint solve for one env (state in registers), u coordinates
+template <int NC>
+__device__ __forceinline__ void dynamics(Slots& S, const float qpos[13], const float u[NV], const float warm_u[NV],
+                                         const float R[9], const float ctrl[3], uint32_t flags, StepResult& out) {
+  DynPre P;
+  dyn_pre(qpos, u, R, P);
+  ScalRows sr;
+  scalar_rows(qpos, u, sr);
+  dyn_post<NC>(S, P, qpos, u, warm_u, R, ctrl, flags, sr, out);
+}
+
 // ------------------------------------------------------------------ state I/O helpers
 template <int SC>
 __device__ __forceinline__ void reset_pose(float qpos[13], float qvel[NV], float warm[NV]) {
@@ -1840,16 +1948,23 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
   return r;
 }
 
+#ifndef AK_XCH
+#define AK_XCH 0  // 1: barrier 0, the observation wave computes the controller and the scalar rows (measured slower: 8.43 -> 9.17 us)
+#endif
+
 template <int NC>
-__device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t* sh_bad, const uint8_t* sh_reset,
-                                              int lane, int e, bool valid, int slot, int npair) {
+__device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, uint8_t* sh_bad,
+                                              const uint8_t* sh_reset, int lane, int e, bool valid, int slot,
+                                              int npair) {
   const int n = A.n;
   Slots S{lds + lane};
   const uint32_t vo = 4u * (uint32_t)e;
   const Soa st = soa(A.state, NSTATE, n);
   float qpos[13], qvel[NV], warm[NV];
-  bool redo = false;
+  bool redo = false, bad_state = false;
   uint32_t step = 0, episode = 0;
+  float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
+  DynPre P;
   if (valid) {
     STAMP(0);
 #pragma unroll
@@ -1860,45 +1975,46 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
     for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
     step = __float_as_uint(ldf(st, ST_STEP, vo));
     episode = __float_as_uint(ldf(st, ST_EPIS, vo));
-    const Soa act = soa(A.action, 2, n);
-    const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
-    float ctrl[3];
-    bool badctrl;
-    controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    if constexpr (!AK_XCH) {
+      const Soa act = soa(A.action, 2, n);
+      const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+      bool badctrl;
+      controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    }
     STAMP(1);
-    bool bad_state = false;
 #pragma unroll
     for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
 #pragma unroll
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
-#pragma unroll 1
-    for (int pass = 0; pass < 2; pass++) {
-      if (bad_state) {
-#pragma unroll
-        for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
-#pragma unroll
-        for (int i = 0; i < NV; i++) { qvel[i] = 0.0f; warm[i] = 0.0f; }
-        ctrl[0] = ctrl[1] = ctrl[2] = 0.0f;
-      }
-      float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
-      normq(q);
-      float R[9];
-      quat_R(q, R);
-      float u[NV], wu[NV];
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        u[k] = R[k] * qvel[0] + R[3 + k] * qvel[1] + R[6 + k] * qvel[2];
-        wu[k] = R[k] * warm[0] + R[3 + k] * warm[1] + R[6 + k] * warm[2];
-      }
-#pragma unroll
-      for (int i = 3; i < NV; i++) { u[i] = qvel[i]; wu[i] = warm[i]; }
-      StepResult res;
-      dynamics<NC>(S, qpos, u, wu, R, ctrl, A.flags, res);
-      if (res.bad && pass == 0) { bad_state = true; redo = true; continue; }
-      euler_advance(u, res, R, qpos, qvel, warm);
-      STAMP(8);
-      break;
+    if (bad_state) reset_to_qpos0(qpos, qvel, warm, ctrl);  // mj_checkPos / mj_checkVel -> mj_resetData
+    to_u(qpos, qvel, warm, R, u, wu);
+    dyn_pre(qpos, u, R, P);
+  }
+  ScalRows sr;
+  if constexpr (AK_XCH) {
+    // barrier 0: wave 1 has put this env's controller output and scalar rows into LDS (computed
+    // from the loaded state; an env reset for a bad state computes its own at qpos0)
+    __syncthreads();
+    float xc[3];
+    xch_get(xch, slot, 64 * npair, sr, xc);
+    if (bad_state) scalar_rows(qpos, u, sr);
+    else {
+      ctrl[0] = xc[0]; ctrl[1] = xc[1]; ctrl[2] = xc[2];
     }
+  } else if (valid) {
+    scalar_rows(qpos, u, sr);
+  }
+  if (valid) {
+    StepResult res;
+    dyn_post<NC>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res);
+    if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
+      bad_state = redo = true;
+      reset_to_qpos0(qpos, qvel, warm, ctrl);
+      to_u(qpos, qvel, warm, R, u, wu);
+      dynamics<NC>(S, qpos, u, wu, R, ctrl, A.flags, res);
+    }
+    euler_advance(u, res, R, qpos, qvel, warm);
+    STAMP(8);
   }
   sh_bad[slot] = redo ? 1 : 0;
   __syncthreads();  // 1: wave 1 has written obs and the auto-reset decisions; it learns the redos
@@ -1921,13 +2037,13 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, uint8_t
   STAMP(10);
 }
 
-__device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
-                                              bool valid, int slot, int npair) {
+__device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, const uint8_t* sh_bad, uint8_t* sh_reset,
+                                              int lane, int e, bool valid, int slot, int npair) {
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
   const Soa st = soa(A.state, NSTATE, n);
   const Soa obs = soa(A.obs, NOBS, n);
-  float qpos[7];
+  float qpos[13];
   float gx = 0.0f, gy = 0.0f, ref[3] = {0.0f, 0.0f, 0.0f};
   uint32_t step = 0;
   bool bad_state = false;
@@ -1935,7 +2051,10 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
   const Soa ep = soa(A.ep, 4, n);
   if (valid) {
 #pragma unroll
-    for (int i = 0; i < 7; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+    float qvel[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
     gx = ldf(st, ST_GOAL, vo);
     gy = ldf(st, ST_GOAL + 1, vo);
 #pragma unroll
@@ -1944,10 +2063,22 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
     if (A.ep) { ep0 = ldf(ep, 0, vo); ep1 = ldf(ep, 1, vo); ep2 = ldf(ep, 2, vo); ep3 = ldf(ep, 3, vo); }
     // mj_checkPos / mj_checkVel on the loaded state (the same test as wave 0's)
 #pragma unroll
-    for (int i = 0; i < 13; i++) bad_state |= is_bad(ldf(st, ST_QPOS + i, vo));
+    for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
 #pragma unroll
-    for (int i = 0; i < NV; i++) bad_state |= is_bad(ldf(st, ST_QVEL + i, vo));
+    for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
+    if constexpr (AK_XCH) {
+      // the dynamics wave's controller and scalar rows (hinge positions / speeds only: u = qvel there)
+      const Soa act = soa(A.action, 2, n);
+      const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+      float ctrl[3];
+      bool badctrl;
+      controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+      ScalRows sr;
+      scalar_rows(qpos, qvel, sr);
+      xch_put(xch, slot, 64 * npair, sr, ctrl);
+    }
   }
+  if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
   const uint32_t nstep = step + 1;
   const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
   ObsOut o{};
@@ -2013,14 +2144,15 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
 template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
+  __shared__ float xch[AK_XCH ? XCH_WORDS * 64 * PW : 1];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int pair = wave % PW, slot = pair * 64 + lane;
   const int e = blockIdx.x * (A.epw * PW) + pair * A.epw + lane;
   const bool valid = lane < A.epw && e < A.n;
-  if (wave < PW) step_dyn_wave<NC>(A, lds, sh_bad, sh_reset, lane, e, valid, slot, PW);
-  else step_obs_wave(A, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  if (wave < PW) step_dyn_wave<NC>(A, lds, xch, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  else step_obs_wave(A, xch, sh_bad, sh_reset, lane, e, valid, slot, PW);
 }
 #ifndef AK_NC_PW
 #define AK_NC_PW 1  // wave pairs per workgroup of the contacts-off kernel
