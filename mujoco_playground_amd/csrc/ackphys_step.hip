@@ -167,6 +167,9 @@ __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }
 #ifndef AK_HWMATH
 #define AK_HWMATH 1
 #endif
+#ifndef AK_POLYTRIG
+#define AK_POLYTRIG 1
+#endif
 #if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
@@ -180,7 +183,21 @@ __device__ __forceinline__ float frsq(float x) { return 1.0f / sqrtf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return sqrtf(x); }
 #define AK_PIVOT_RSQ(x) __frsqrt_rn(x)
 #endif
-__device__ __forceinline__ void fsincos(float x, float& s, float& c) { sincosf(x, &s, &c); }
+// sin / cos: the kernels' arguments are steer angles (|x| < ~0.7) and half rotation angles of one
+// step (|x| << 1), so when every lane's |x| <= pi/4 the wave takes the Cephes minimax polynomials of
+// that interval (the ones sincosf itself uses after its range reduction); otherwise sincosf.
+__device__ __forceinline__ void fsincos(float x, float& s, float& c) {
+#if AK_POLYTRIG
+  if (__builtin_amdgcn_ballot_w64(!(fabsf(x) <= 0.785398163f)) == 0ull) {
+    const float z = x * x;
+    s = fmaf(x * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), x);
+    c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+             fmaf(-0.5f, z, 1.0f));
+    return;
+  }
+#endif
+  sincosf(x, &s, &c);
+}
 // wrap to [-pi, pi] (atan2(sin a, cos a) of the reference) for |a| <= 3 pi
 __device__ __forceinline__ float wrap_pi(float a) {
   return fmaf(__builtin_rintf(a * 0.159154943091895336f), -6.28318530717958648f, a);
