@@ -80,6 +80,13 @@ def main():
             if quad:
                 its = its.reshape(nb, 64)[:, :16].reshape(-1)
             if k == 200:
+                ls = its >> 8
+                its = its & 0xFF
+                if quad:
+                    lsw = ls.reshape(nb, -1).max(axis=1)
+                    print(f"  line-search phi' evaluations per lane: mean {ls.mean():.2f} (per Newton iteration "
+                          f"{ls.sum() / max((its // 8).sum(), 1):.2f}), hist {np.bincount(ls, minlength=4)[:20]}, "
+                          f"wave-max hist {np.bincount(lsw, minlength=4)[:30]}")
                 itn, why = its // 8, its % 8
                 wmax = itn.reshape(nb, -1).max(axis=1)
                 print(f"  iterations: lane mean {itn.mean():.2f}, lane hist {np.bincount(itn, minlength=13)}, "
