@@ -1966,11 +1966,11 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 }
 
 #ifndef AK_XCH
-#define AK_XCH 0  // 1: barrier 0, the observation wave computes the controller and the scalar rows (measured slower: 8.43 -> 9.17 us)
+#define AK_XCH 1  // a third "prep" wave computes the controller and the scalar rows (LDS + flag)
 #endif
 
 template <int NC>
-__device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, uint8_t* sh_bad,
+__device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
                                               const uint8_t* sh_reset, int lane, int e, bool valid, int slot,
                                               int npair) {
   const int n = A.n;
@@ -1982,6 +1982,10 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   uint32_t step = 0, episode = 0;
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
+  if constexpr (AK_XCH) {
+    if (lane == 0) *xflag = 0;
+    __syncthreads();  // barrier 0: the exchange flag is clear before the prep wave can raise it
+  }
   if (valid) {
     STAMP(0);
 #pragma unroll
@@ -2009,11 +2013,11 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   }
   ScalRows sr;
   if constexpr (AK_XCH) {
-    // barrier 0: wave 1 has put this env's controller output and scalar rows into LDS (computed
-    // from the loaded state; an env reset for a bad state computes its own at qpos0)
-    __syncthreads();
+    // the prep wave has put this env's controller output and scalar rows into LDS (computed from
+    // the loaded state; an env reset for a bad state computes its own at qpos0): wait for its flag
+    while (__hip_atomic_load(xflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
     float xc[3];
-    xch_get(xch, slot, 64 * npair, sr, xc);
+    xch_get(xch, slot, 64, sr, xc);
     if (bad_state) scalar_rows(qpos, u, sr);
     else {
       ctrl[0] = xc[0]; ctrl[1] = xc[1]; ctrl[2] = xc[2];
@@ -2054,8 +2058,9 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   STAMP(10);
 }
 
-__device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, const uint8_t* sh_bad, uint8_t* sh_reset,
-                                              int lane, int e, bool valid, int slot, int npair) {
+__device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
+                                              bool valid, int slot, int npair) {
+  if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
   const Soa st = soa(A.state, NSTATE, n);
@@ -2083,19 +2088,7 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, const u
     for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
 #pragma unroll
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
-    if constexpr (AK_XCH) {
-      // the dynamics wave's controller and scalar rows (hinge positions / speeds only: u = qvel there)
-      const Soa act = soa(A.action, 2, n);
-      const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
-      float ctrl[3];
-      bool badctrl;
-      controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
-      ScalRows sr;
-      scalar_rows(qpos, qvel, sr);
-      xch_put(xch, slot, 64 * npair, sr, ctrl);
-    }
   }
-  if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
   const uint32_t nstep = step + 1;
   const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
   ObsOut o{};
@@ -2156,27 +2149,65 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
   step_serial(A, lds, lane, e);
 }
 
+// Prep wave (AK_XCH): the controller (float64) and the scalar constraint rows of the same 64 envs,
+// off the dynamics wave's critical path -- they need only the action and the hinge positions and
+// speeds. Handed over through LDS and a workgroup-scope release / acquire flag (no barrier: the
+// observation wave must not wait for it); then the wave joins barriers 1 and 2 and exits.
+__device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad, int lane,
+                                               int e, bool valid) {
+  __syncthreads();  // barrier 0 (see step_dyn_wave)
+  if (valid) {
+    const int n = A.n;
+    const uint32_t vo = 4u * (uint32_t)e;
+    const Soa st = soa(A.state, NSTATE, n);
+    float qpos[13], qvel[NV];
+#pragma unroll
+    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+    const Soa act = soa(A.action, 2, n);
+    const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+    float ctrl[3];
+    bool badctrl;
+    controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    ScalRows sr;
+    scalar_rows(qpos, qvel, sr);  // hinge dofs only: u = qvel there
+    xch_put(xch, lane, 64, sr, ctrl);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every lane's exchange words before the flag
+  if (lane == 0) __hip_atomic_store(xflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();                                                           // barrier 1
+  if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, 1)) != 0ull) __syncthreads();  // barrier 2
+}
+
 // PW wave pairs per workgroup: waves 0..PW-1 run the dynamics of envs [64 w, 64 w + 64) of the
-// block, waves PW..2PW-1 their observations (2 PW waves on the CU's 4 SIMDs)
+// block, waves PW..2PW-1 their observations (2 PW waves on the CU's 4 SIMDs); with AK_XCH a
+// third wave (PW = 1) prepares the controller and scalar rows
 template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
+  static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ float xch[AK_XCH ? XCH_WORDS * 64 * PW : 1];
+  __shared__ float xch[AK_XCH ? XCH_WORDS * 64 : 1];
+  __shared__ int xflag[1];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int pair = wave % PW, slot = pair * 64 + lane;
   const int e = blockIdx.x * (A.epw * PW) + pair * A.epw + lane;
   const bool valid = lane < A.epw && e < A.n;
-  if (wave < PW) step_dyn_wave<NC>(A, lds, xch, sh_bad, sh_reset, lane, e, valid, slot, PW);
-  else step_obs_wave(A, xch, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  if (wave < PW) step_dyn_wave<NC>(A, lds, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  else if (wave < 2 * PW) step_obs_wave(A, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  else step_prep_wave(A, xch, xflag, sh_bad, lane, blockIdx.x * A.epw + lane, lane < A.epw && blockIdx.x * A.epw + lane < A.n);
 }
 #ifndef AK_NC_PW
 #define AK_NC_PW 1  // wave pairs per workgroup of the contacts-off kernel
 #endif
-extern "C" __global__ void __launch_bounds__(128, 1) ackphys_step_kernel(Args A) { step_split<0, 1>(A); }
+constexpr int LANE_THREADS = 64 * (2 * AK_NC_PW + (AK_XCH ? 1 : 0));
+extern "C" __global__ void __launch_bounds__(64 * (2 + (AK_XCH ? 1 : 0)), 1) ackphys_step_kernel(Args A) {
+  step_split<0, 1>(A);
+}
 // contacts off (BASELINE configs[1]): the contact machinery is compiled out
-extern "C" __global__ void __launch_bounds__(128 * AK_NC_PW, 1) ackphys_step_nc_kernel(Args A) {
+extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_kernel(Args A) {
   step_split<1, AK_NC_PW>(A);
 }
 
@@ -2370,9 +2401,10 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else if (flags & ACKPHYS_CONTACTS)
-      hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64 * (2 + (AK_XCH ? 1 : 0))), 0, (hipStream_t)stream,
+                         a);
     else
-      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(128 * pw), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(LANE_THREADS), 0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");
