@@ -384,9 +384,15 @@ __device__ __forceinline__ void ref_kb(float& K, float& B) { ref_kb_p(SOLREF[0],
 #include "ackphys_scene.inc"
 
 // writes the 79 observation words of one env to dst (stride n); returns reward/term/etc.
-template <int SC>
+struct NoPreMin {
+  __device__ __forceinline__ float operator()() const { return 3.0e38f; }
+};
+// RFIRST > 10: rays 10 .. RFIRST-1 were cast (and stored) by another wave, whose minimum reading
+// `premin()` returns once it is available
+template <int SC, int RFIRST = 10, class PreMin = NoPreMin>
 __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], const float R[9], float gx, float gy,
-                          const float ref[3], const Soa& dst, uint32_t vo, const EnvParams& prm) {
+                          const float ref[3], const Soa& dst, uint32_t vo, const EnvParams& prm,
+                          const PreMin& premin = PreMin{}) {
   float head[7];
   ObsOut o = observe_head(p, q, R, gx, gy, ref, head, prm);
   STAMP(11);
@@ -395,7 +401,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   float minl = 3.0e38f, v71 = -1.0f;
   const RayFrame F = ray_frame(p, R);
 #pragma unroll
-  for (int i = 10; i < 72; i++) {
+  for (int i = RFIRST; i < 72; i++) {
     float v;
     if constexpr (SC == 0) v = ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
     else v = ray_scene<SC>(F, RAY_DIR[i][0], RAY_DIR[i][1]);
@@ -408,6 +414,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   for (int i = 0; i < 10; i++) stf(dst, i, vo, v71);
 #pragma unroll
   for (int k = 0; k < 7; k++) stf(dst, 72 + k, vo, head[k]);
+  if constexpr (RFIRST > 10) minl = fminf(minl, premin());
   o.minl = minl;
   o.coll = minl < prm.collision_threshold;
   float r = 0.0f;
@@ -1968,6 +1975,10 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 #ifndef AK_XCH
 #define AK_XCH 1  // a third "prep" wave computes the controller and the scalar rows (LDS + flag)
 #endif
+#ifndef AK_PREP_RAYS
+#define AK_PREP_RAYS 30  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
+#endif
+static_assert(AK_XCH || AK_PREP_RAYS == 10, "prep rays need the prep wave");
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
@@ -1983,8 +1994,8 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
   if constexpr (AK_XCH) {
-    if (lane == 0) *xflag = 0;
-    __syncthreads();  // barrier 0: the exchange flag is clear before the prep wave can raise it
+    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; }
+    __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
   if (valid) {
     STAMP(0);
@@ -2058,8 +2069,8 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   STAMP(10);
 }
 
-__device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_bad, uint8_t* sh_reset, int lane, int e,
-                                              bool valid, int slot, int npair) {
+__device__ __forceinline__ void step_obs_wave(const Args& A, const float* xch, int* xflag, const uint8_t* sh_bad,
+                                              uint8_t* sh_reset, int lane, int e, bool valid, int slot, int npair) {
   if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
@@ -2105,7 +2116,16 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const uint8_t* sh_b
       normq(q);
       float R[9];
       quat_R(q, R);
-      o = observe<0>(p, q, R, gx, gy, ref, obs, vo, A.prm);
+      if (pass == 0) {
+        o = observe<0, AK_PREP_RAYS>(p, q, R, gx, gy, ref, obs, vo, A.prm, [&]() __attribute__((always_inline)) {
+          // the prep wave's rays: written to obs and their minimum to LDS before it raised flag 1
+          while (__hip_atomic_load(xflag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            __builtin_amdgcn_s_sleep(1);
+          return xch[XCH_WORDS * 64 + lane];
+        });
+      } else {
+        o = observe<0>(p, q, R, gx, gy, ref, obs, vo, A.prm);  // redone env: every ray at qpos0
+      }
       stf(soa(A.reward, 1, n), 0, vo, o.reward);
       stb(soa(A.term, 1, n, 1), (uint32_t)e, o.term ? 1 : 0);
       stb(soa(A.trunc, 1, n, 1), (uint32_t)e, trunc ? 1 : 0);
@@ -2176,6 +2196,44 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every lane's exchange words before the flag
   if (lane == 0) __hip_atomic_store(xflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if constexpr (AK_PREP_RAYS > 10) {
+    // rangefinders 10 .. AK_PREP_RAYS-1 of the observation (taken at the pre-integration pose, or at
+    // qpos0 for a state mj_checkPos/Vel resets): stored here, their minimum handed to wave 1
+    float mn = 3.0e38f;
+    if (valid) {
+      const int n = A.n;
+      const uint32_t vo = 4u * (uint32_t)e;
+      const Soa st = soa(A.state, NSTATE, n);
+      float pq[7];
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < 7; i++) pq[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+      for (int i = 0; i < 13; i++) bad |= is_bad(ldf(st, ST_QPOS + i, vo));
+#pragma unroll
+      for (int i = 0; i < NV; i++) bad |= is_bad(ldf(st, ST_QVEL + i, vo));
+      if (bad) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) pq[i] = QPOS0[i];
+      }
+      const float p[3] = {pq[0], pq[1], pq[2]};
+      float q[4] = {pq[3], pq[4], pq[5], pq[6]};
+      normq(q);
+      float R[9];
+      quat_R(q, R);
+      const Soa obs = soa(A.obs, NOBS, n);
+#pragma unroll
+      for (int i = 10; i < AK_PREP_RAYS; i++) {
+        const float v = ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
+        stf(obs, i, vo, v);
+        mn = fminf(mn, v);
+      }
+    }
+    xch[XCH_WORDS * 64 + lane] = mn;
+    __builtin_amdgcn_s_waitcnt(0);  // the observation rows are written (wave 1 may copy them as terminal obs)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   __syncthreads();                                                           // barrier 1
   if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, 1)) != 0ull) __syncthreads();  // barrier 2
 }
@@ -2187,8 +2245,8 @@ template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
   static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ float xch[AK_XCH ? XCH_WORDS * 64 : 1];
-  __shared__ int xflag[1];
+  __shared__ float xch[AK_XCH ? (XCH_WORDS + 1) * 64 : 1];
+  __shared__ int xflag[2];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -2196,7 +2254,7 @@ __device__ __forceinline__ void step_split(const Args& A) {
   const int e = blockIdx.x * (A.epw * PW) + pair * A.epw + lane;
   const bool valid = lane < A.epw && e < A.n;
   if (wave < PW) step_dyn_wave<NC>(A, lds, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
-  else if (wave < 2 * PW) step_obs_wave(A, sh_bad, sh_reset, lane, e, valid, slot, PW);
+  else if (wave < 2 * PW) step_obs_wave(A, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
   else step_prep_wave(A, xch, xflag, sh_bad, lane, blockIdx.x * A.epw + lane, lane < A.epw && blockIdx.x * A.epw + lane < A.n);
 }
 #ifndef AK_NC_PW
