@@ -25,15 +25,32 @@
 
 // Diagnostic build only (-DAK_STAMPS): per-wave s_memtime phase stamps, never in the product.
 #ifdef AK_STAMPS
+// layout: [AK_NSTAMP][blocks] phase stamps, [blocks][64] Newton iteration counts, [5][blocks] Newton phases
+#define AK_NSTAMP 24
 __device__ unsigned long long* g_stamps;
+// The stamps are kept in LDS (one row per wave) and written out when the wave leaves its role
+// function: a global store per stamp would add a pointer load and a vmcnt(0) wait to every stamp.
+__shared__ unsigned long long ak_stamp_lds[4][AK_NSTAMP];
 #define STAMP(k)                                                                          \
   do {                                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                                    \
     unsigned long long _t;                                                                \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
     __builtin_amdgcn_sched_barrier(0);                                                    \
-    if ((threadIdx.x & 63) == 0) g_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;       \
+    if ((threadIdx.x & 63) == 0) ak_stamp_lds[threadIdx.x >> 6][k] = _t;                  \
   } while (0)
+struct StampScope {
+  __device__ StampScope() {
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < AK_NSTAMP; k++) ak_stamp_lds[threadIdx.x >> 6][k] = 0;
+  }
+  __device__ ~StampScope() {
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < AK_NSTAMP; k++)
+        if (const unsigned long long v = ak_stamp_lds[threadIdx.x >> 6][k]) g_stamps[(size_t)k * gridDim.x + blockIdx.x] = v;
+  }
+};
+#define STAMP_SCOPE StampScope _stamp_scope;
 // Newton-phase accumulators (diag build): NT_MARK(ph) adds the cycles since the previous mark to phase ph
 #define NT_DECL unsigned long long _nt_acc[5] = {0, 0, 0, 0, 0}, _nt_last = 0;
 #define NT_NOW(v)                                                                \
@@ -54,13 +71,14 @@ __device__ unsigned long long* g_stamps;
   do {                                                                                                        \
     if ((threadIdx.x & 63) == 0)                                                                              \
       for (int _p = 0; _p < 5; _p++)                                                                          \
-        g_stamps[(16 + 64 + _p) * (size_t)gridDim.x + blockIdx.x] = _nt_acc[_p];                              \
+        g_stamps[(AK_NSTAMP + 64 + _p) * (size_t)gridDim.x + blockIdx.x] = _nt_acc[_p];                              \
   } while (0)
 #else
 #define NT_DECL
 #define NT_START
 #define NT_MARK(ph)
 #define NT_FLUSH
+#define STAMP_SCOPE
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -357,14 +375,22 @@ __device__ __forceinline__ float ray_floor_f(const RayFrame& F, float dxb, float
 }
 
 // ------------------------------------------------------------------ impedance / reference
+// x^p: small integer powers (solimp's default power 2 in both models) as products -- powf is the
+// device library's general routine (~150 instructions, not folded for a constant exponent)
+__device__ __forceinline__ float fpow(float x, float p) {
+  if (p == 1.0f) return x;
+  if (p == 2.0f) return x * x;
+  if (p == 3.0f) return x * x * x;
+  return powf(x, p);
+}
 __device__ __forceinline__ float impedance_p(float pos, float d0, float dmax, float width, float mid, float pw) {
   // getimpedance: solimp (d0, dmax, width, mid, power), margin 0
   float x = fabsf(pos) * (1.0f / width);
   if (x >= 1.0f) return dmax;
   float y;
   if (pw == 1.0f) y = x;
-  else if (x <= mid) y = powf(x, pw) / powf(mid, pw - 1.0f);
-  else y = 1.0f - powf(1.0f - x, pw) / powf(1.0f - mid, pw - 1.0f);
+  else if (x <= mid) y = fpow(x, pw) / fpow(mid, pw - 1.0f);
+  else y = 1.0f - fpow(1.0f - x, pw) / fpow(1.0f - mid, pw - 1.0f);
   float imp = d0 + y * (dmax - d0);
   return fminf(fmaxf(imp, 0.0001f), 0.9999f);
 }
@@ -1265,6 +1291,65 @@ __device__ __forceinline__ void xch_get(const float* x, int slot, int stride, Sc
   for (int k = 0; k < 3; k++) ctrl[k] = x[(w++) * stride + slot];
 }
 
+// The implicit-Euler factor chol(M + h diag(damping)) depends on the steer angles alone (M is
+// constant but for the front spin axes), so the prep wave computes it beside the solve and hands
+// its structural nonzeros over (float4 per lane: 16-byte LDS reads, conflict-free).
+constexpr int eu_words() {
+  int n = 0;
+  for (int i = 0; i < NV; i++)
+    for (int j = 0; j <= i; j++) n += LPAT[LANE_K(0)].nz[i][j] ? 1 : 0;
+  return n;
+}
+constexpr int EU_VEC = (eu_words() + 3) / 4;
+__device__ __forceinline__ void euler_factor(const float qpos[13], float L[NV][NV]) {
+  float sa[2][3];
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    float c, sn;
+    fsincos(qpos[W_STEER_QPOS[2 + s]], sn, c);
+    rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
+  }
+  build_M(L, sa);
+#pragma unroll
+  for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
+  chol_sp<LANE_K(0)>(L);
+}
+__device__ __forceinline__ void eu_put(float* x, int lane, const float L[NV][NV]) {
+  float w[4 * EU_VEC];
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++)
+      if (LPAT[LANE_K(0)].nz[i][j]) w[n++] = AK_F(L, i, j);
+#pragma unroll
+  for (int k = n; k < 4 * EU_VEC; k++) w[k] = 0.0f;
+  float4* x4 = reinterpret_cast<float4*>(x);
+#pragma unroll
+  for (int v = 0; v < EU_VEC; v++) x4[v * 64 + lane] = make_float4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
+}
+__device__ __forceinline__ void eu_get(const float* x, int lane, float L[NV][NV]) {
+  float w[4 * EU_VEC];
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+#pragma unroll
+  for (int v = 0; v < EU_VEC; v++) {
+    const float4 t = x4[v * 64 + lane];
+    w[4 * v] = t.x; w[4 * v + 1] = t.y; w[4 * v + 2] = t.z; w[4 * v + 3] = t.w;
+  }
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++)
+      if (LPAT[LANE_K(0)].nz[i][j]) AK_F(L, i, j) = w[n++];
+}
+// where the dynamics wave finds the prep wave's Euler factor (XEU): LDS words, flag, lane
+struct EuHand {
+  const float* x;
+  int* flag;
+  int lane;
+};
+
 // forward dynamics, first part (no control): steer-dependent axes, mass matrix, bias, passive
 struct DynPre {
   float sa[2][3], cyl[2][3];
@@ -1290,10 +1375,10 @@ __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV],
 }
 
 // forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
-template <int NC>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
+template <int NC, bool XEU = false>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
 __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
                                          const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
-                                         const ScalRows& sr, StepResult& out) {
+                                         const ScalRows& sr, StepResult& out, EuHand eh = EuHand{}) {
   float(&sa)[2][3] = P.sa;
   float(&cyl)[2][3] = P.cyl;
   Solver& sv = P.sv;
@@ -1725,7 +1810,7 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
   STAMP(6);
   NT_FLUSH;
 #ifdef AK_STAMPS
-  g_stamps[16 * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] = (unsigned long long)(it_done * 8 + why);
+  g_stamps[AK_NSTAMP * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] = (unsigned long long)(it_done * 8 + why);
 #else
   (void)it_done;
   (void)why;
@@ -1751,13 +1836,20 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
   }
   if constexpr (!NC) { FOR_CHAINS(slot_loop_force, S, dirs, sa, fc); }
   // implicit damping Euler: (M + h diag(B)) acc = fs + fc
+  if constexpr (XEU) {  // factored by the prep wave (same steer angles): wait for its flag
+    STAMP(17);
+    while (__hip_atomic_load(eh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+    STAMP(18);
+    eu_get(eh.x, eh.lane, L);
+  } else {
 #pragma unroll
-  for (int i = 0; i < NV; i++)
+    for (int i = 0; i < NV; i++)
 #pragma unroll
-    for (int j = 0; j < NV; j++) L[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
+      for (int j = 0; j < NV; j++) L[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
 #pragma unroll
-  for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
-  chol_sp<LANE_K(0)>(L);
+    for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
+    chol_sp<LANE_K(0)>(L);
+  }
 #pragma unroll
   for (int i = 0; i < NV; i++) out.acce[i] = sv.fs[i] + fc[i];
   chol_sp_solve<LANE_K(0)>(L, out.acce);
@@ -1842,6 +1934,7 @@ using namespace ak;
 // The whole step of one env on one lane, observation included (F_POSTSTEP_OBS: obs/reward need the
 // integrated pose, so nothing can run beside the dynamics).
 __device__ __forceinline__ void step_serial(const Args& A, float* lds, int lane, int e) {
+  STAMP_SCOPE
   const int n = A.n;
   STAMP(0);
   Slots S{lds + lane};
@@ -1975,15 +2068,20 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 #ifndef AK_XCH
 #define AK_XCH 1  // a third "prep" wave computes the controller and the scalar rows (LDS + flag)
 #endif
-#ifndef AK_PREP_RAYS
-#define AK_PREP_RAYS 30  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
+#ifndef AK_XEU
+#define AK_XEU 0  // with AK_XCH: the prep wave also factors M + h diag(damping) for the Euler solve
 #endif
-static_assert(AK_XCH || AK_PREP_RAYS == 10, "prep rays need the prep wave");
+#ifndef AK_PREP_RAYS
+#define AK_PREP_RAYS 40  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
+#endif
+static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU), "prep rays and the Euler factor need the prep wave");
+constexpr int XEU_OFF = (XCH_WORDS + 1) * 64;  // float offset of the Euler factor words in xch
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
                                               const uint8_t* sh_reset, int lane, int e, bool valid, int slot,
                                               int npair) {
+  STAMP_SCOPE
   const int n = A.n;
   Slots S{lds + lane};
   const uint32_t vo = 4u * (uint32_t)e;
@@ -1994,7 +2092,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
   if constexpr (AK_XCH) {
-    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; }
+    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; }
     __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
   if (valid) {
@@ -2026,7 +2124,9 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   if constexpr (AK_XCH) {
     // the prep wave has put this env's controller output and scalar rows into LDS (computed from
     // the loaded state; an env reset for a bad state computes its own at qpos0): wait for its flag
+    STAMP(20);
     while (__hip_atomic_load(xflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+    STAMP(15);
     float xc[3];
     xch_get(xch, slot, 64, sr, xc);
     if (bad_state) scalar_rows(qpos, u, sr);
@@ -2038,7 +2138,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   }
   if (valid) {
     StepResult res;
-    dyn_post<NC>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res);
+    dyn_post<NC, AK_XEU != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res, EuHand{xch + XEU_OFF, xflag + 2, lane});
     if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
       bad_state = redo = true;
       reset_to_qpos0(qpos, qvel, warm, ctrl);
@@ -2071,6 +2171,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
 
 __device__ __forceinline__ void step_obs_wave(const Args& A, const float* xch, int* xflag, const uint8_t* sh_bad,
                                               uint8_t* sh_reset, int lane, int e, bool valid, int slot, int npair) {
+  STAMP_SCOPE
   if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
@@ -2121,6 +2222,7 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const float* xch, i
           // the prep wave's rays: written to obs and their minimum to LDS before it raised flag 1
           while (__hip_atomic_load(xflag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
             __builtin_amdgcn_s_sleep(1);
+          STAMP(19);
           return xch[XCH_WORDS * 64 + lane];
         });
       } else {
@@ -2172,15 +2274,20 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
 // Prep wave (AK_XCH): the controller (float64) and the scalar constraint rows of the same 64 envs,
 // off the dynamics wave's critical path -- they need only the action and the hinge positions and
 // speeds. Handed over through LDS and a workgroup-scope release / acquire flag (no barrier: the
-// observation wave must not wait for it); then the wave joins barriers 1 and 2 and exits.
+// observation wave must not wait for it). Then (AK_XEU) the implicit-Euler factor, which the
+// dynamics wave needs only after its solve (flag 2), and (AK_PREP_RAYS) rangefinders for the
+// observation wave (flag 1); the wave joins barriers 1 and 2 and exits.
 __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad, int lane,
                                                int e, bool valid) {
+  STAMP_SCOPE
   __syncthreads();  // barrier 0 (see step_dyn_wave)
+  const int n = A.n;
+  const uint32_t vo = 4u * (uint32_t)e;
+  const Soa st = soa(A.state, NSTATE, n);
+  float qpos[13];
+  bool bad = false;
   if (valid) {
-    const int n = A.n;
-    const uint32_t vo = 4u * (uint32_t)e;
-    const Soa st = soa(A.state, NSTATE, n);
-    float qpos[13], qvel[NV];
+    float qvel[NV];
 #pragma unroll
     for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
 #pragma unroll
@@ -2189,35 +2296,43 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
     const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
     float ctrl[3];
     bool badctrl;
+    STAMP(21);
     controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    STAMP(22);
     ScalRows sr;
     scalar_rows(qpos, qvel, sr);  // hinge dofs only: u = qvel there
+    STAMP(23);
     xch_put(xch, lane, 64, sr, ctrl);
+    // mj_checkPos / mj_checkVel (the dynamics wave's test): a reset state is factored / observed at qpos0
+#pragma unroll
+    for (int i = 0; i < 13; i++) bad |= is_bad(qpos[i]);
+#pragma unroll
+    for (int i = 0; i < NV; i++) bad |= is_bad(qvel[i]);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every lane's exchange words before the flag
   if (lane == 0) __hip_atomic_store(xflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  STAMP(13);
+  if (valid && bad) {
+#pragma unroll
+    for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+  }
+  if constexpr (AK_XEU) {
+    if (valid) {
+      float L[NV][NV];
+      euler_factor(qpos, L);
+      eu_put(xch + XEU_OFF, lane, L);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    STAMP(16);
+  }
   if constexpr (AK_PREP_RAYS > 10) {
     // rangefinders 10 .. AK_PREP_RAYS-1 of the observation (taken at the pre-integration pose, or at
     // qpos0 for a state mj_checkPos/Vel resets): stored here, their minimum handed to wave 1
     float mn = 3.0e38f;
     if (valid) {
-      const int n = A.n;
-      const uint32_t vo = 4u * (uint32_t)e;
-      const Soa st = soa(A.state, NSTATE, n);
-      float pq[7];
-      bool bad = false;
-#pragma unroll
-      for (int i = 0; i < 7; i++) pq[i] = ldf(st, ST_QPOS + i, vo);
-#pragma unroll
-      for (int i = 0; i < 13; i++) bad |= is_bad(ldf(st, ST_QPOS + i, vo));
-#pragma unroll
-      for (int i = 0; i < NV; i++) bad |= is_bad(ldf(st, ST_QVEL + i, vo));
-      if (bad) {
-#pragma unroll
-        for (int i = 0; i < 7; i++) pq[i] = QPOS0[i];
-      }
-      const float p[3] = {pq[0], pq[1], pq[2]};
-      float q[4] = {pq[3], pq[4], pq[5], pq[6]};
+      const float p[3] = {qpos[0], qpos[1], qpos[2]};
+      float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
       normq(q);
       float R[9];
       quat_R(q, R);
@@ -2233,6 +2348,7 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
     __builtin_amdgcn_s_waitcnt(0);  // the observation rows are written (wave 1 may copy them as terminal obs)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(xflag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    STAMP(14);
   }
   __syncthreads();                                                           // barrier 1
   if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, 1)) != 0ull) __syncthreads();  // barrier 2
@@ -2245,8 +2361,8 @@ template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
   static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ float xch[AK_XCH ? (XCH_WORDS + 1) * 64 : 1];
-  __shared__ int xflag[2];
+  __shared__ __attribute__((aligned(16))) float xch[AK_XCH ? XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0) : 1];
+  __shared__ int xflag[3];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;

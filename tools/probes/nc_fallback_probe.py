@@ -10,6 +10,7 @@ import sys
 import numpy as np
 import torch
 
+NSTAMP = 24  # AK_NSTAMP of the diagnostic build
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -31,7 +32,7 @@ def main():
     p = lambda t: P(t.data_ptr())
     stream = P(torch.cuda.current_stream().cuda_stream)
     nb = (n + 63) // 64
-    stamps = torch.zeros(16 * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(NSTAMP * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(p(stamps)) == 0
     obs = torch.zeros(79, n, device=dev)
     rew = torch.zeros(n, device=dev)
@@ -44,7 +45,7 @@ def main():
     assert L.ackphys_create(blob, len(blob), n4, 0, C.byref(ctx4)) == 0
     assert L.ackphys_set_variant(ctx4, 0) == 0
     nb4 = (n4 + 63) // 64
-    st4 = torch.zeros(16 * nb4 + nb4 * 64 + 5 * nb4, dtype=torch.int64, device=dev)
+    st4 = torch.zeros(NSTAMP * nb4 + nb4 * 64 + 5 * nb4, dtype=torch.int64, device=dev)
     state4, obs4 = torch.zeros(44, n4, device=dev), torch.zeros(79, n4, device=dev)
     rew4, term4, trunc4 = (torch.zeros(n4, device=dev), torch.zeros(n4, dtype=torch.uint8, device=dev),
                            torch.zeros(n4, dtype=torch.uint8, device=dev))
@@ -57,7 +58,7 @@ def main():
         L.ackphys_step(ctx4, p(acts4[k]), p(state4), p(obs4), p(rew4), p(term4), p(trunc4), None, None, None, 2, 0,
                        stream)
         torch.cuda.synchronize()
-        it = st4.cpu().numpy()[16 * nb4: 16 * nb4 + 64 * nb4] // 8
+        it = st4.cpu().numpy()[NSTAMP * nb4: NSTAMP * nb4 + 64 * nb4] // 8
         w = it.reshape(-1, 64).max(1)
         print(f"bench step {k}: lane hist {np.bincount(it, minlength=4)[:6]} wave-max hist {np.bincount(w, minlength=4)[:6]}")
     assert L.ackphys_diag_set_stamps(p(stamps)) == 0
@@ -81,7 +82,7 @@ def main():
             L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, 2, seed,
                            stream)
             torch.cuda.synchronize()
-            it = stamps.cpu().numpy()[16 * nb: 16 * nb + 64 * nb] // 8
+            it = stamps.cpu().numpy()[NSTAMP * nb: NSTAMP * nb + 64 * nb] // 8
             print(f"seed {seed} step {k}: Newton iterations after the predicted piece, lane hist "
                   f"{np.bincount(it, minlength=4)[:8]}")
 

@@ -12,6 +12,7 @@ import sys
 import numpy as np
 import torch
 
+NSTAMP = 24  # AK_NSTAMP of the diagnostic build
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
@@ -21,6 +22,15 @@ PHASES = [(0, 1, "load+controller"), (1, 2, "kin->dyn"), (2, 3, "M/bias/a0"), (3
           (8, 9, "barriers"), (9, 10, "state store"), (11, 12, "obs wave: rays")]
 
 
+# contacts-off kernel: when each event happens, cycles after the dynamics wave's first stamp
+TIMELINE = [(1, "dyn: state loaded"), (21, "prep: loads issued"), (22, "prep: controller done"),
+            (23, "prep: rows done"), (20, "dyn: waits for prep words"), (13, "prep: ctrl+rows published"),
+            (15, "dyn: prep words received"), (11, "obs: head done"), (16, "prep: Euler factor published"),
+            (17, "dyn: waits for Euler factor"), (18, "dyn: Euler factor received"), (12, "obs: own rays done"),
+            (14, "prep: rays published"), (19, "obs: prep rays received"), (7, "dyn: dynamics done"),
+            (8, "dyn: integrated"), (9, "dyn: past barriers"), (10, "dyn: state stored")]
+
+
 QUAD_PHASES = [(0, 1, "load+controller"), (1, 2, "kinematics"), (2, 3, "M/bias/a0"), (3, 4, "contacts"),
                (4, 5, "rows"), (5, 6, "newton"), (6, 10, "post-newton")]
 
@@ -28,7 +38,7 @@ QUAD_PHASES = [(0, 1, "load+controller"), (1, 2, "kinematics"), (2, 3, "M/bias/a
 def main():
     quad = len(sys.argv) > 1 and sys.argv[1] == "quad"
     phases = QUAD_PHASES if quad else PHASES
-    L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", "libackphys_stamps.so"))
+    L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", os.environ.get("DIAG_LIB", "libackphys_stamps.so")))
     P = C.c_void_p
     L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
     L.ackphys_step.argtypes = [P] * 10 + [C.c_uint32, C.c_uint64, P]
@@ -48,7 +58,7 @@ def main():
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
     nb = (n + 15) // 16 if quad else (n + 63) // 64
-    stamps = torch.zeros(16 * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(NSTAMP * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
     p = lambda t: P(t.data_ptr())
     stream = P(torch.cuda.current_stream().cuda_stream)
@@ -68,11 +78,11 @@ def main():
                            stream)
             torch.cuda.synchronize()
             allv = stamps.cpu().numpy()
-            s = allv[: 16 * nb].reshape(16, nb)
+            s = allv[: NSTAMP * nb].reshape(NSTAMP, nb)
             res.append(np.stack([s[b] - s[a] for a, b, _ in phases]))
             spans.append(s[10] - s[0] if not quad else np.sum(res[-1], axis=0))
-            its = allv[16 * nb:16 * nb + 64 * nb]
-            nt = allv[16 * nb + 64 * nb:].reshape(5, nb)
+            its = allv[NSTAMP * nb:NSTAMP * nb + 64 * nb]
+            nt = allv[NSTAMP * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
                 print("  newton phases (median cycles/wave, summed over iterations): " + ", ".join(
                     f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"])))
@@ -92,6 +102,9 @@ def main():
                 print(f"  iterations: lane mean {itn.mean():.2f}, lane hist {np.bincount(itn, minlength=13)}, "
                       f"wave-max hist {np.bincount(wmax, minlength=13)}, exit reasons (1 exact,2 grad,3 nodesc,4 maxit) "
                       f"{np.bincount(why, minlength=5)[1:]}")
+            if not quad and k == 200 and flags == 2:
+                print("  timeline (median cycles after the dynamics wave's first stamp): " + ", ".join(
+                    f"{nm} {np.median(s[i] - s[0]):.0f}" for i, nm in TIMELINE if s[i].any()))
         d = np.median(np.concatenate(res, axis=1), axis=1)
         tot = np.median(np.concatenate(spans))
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
