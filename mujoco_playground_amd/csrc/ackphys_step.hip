@@ -2069,7 +2069,7 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 #define AK_XCH 1  // a third "prep" wave computes the controller and the scalar rows (LDS + flag)
 #endif
 #ifndef AK_XEU
-#define AK_XEU 0  // with AK_XCH: the prep wave also factors M + h diag(damping) for the Euler solve
+#define AK_XEU 1  // with AK_XCH: the prep wave also factors M + h diag(damping) for the Euler solve
 #endif
 #ifndef AK_PREP_RAYS
 #define AK_PREP_RAYS 40  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
