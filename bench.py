@@ -285,12 +285,14 @@ def main():
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     valu = None
     if pmc and pmc.get("valu_insts_per_wave"):
-        # one wave alone issues a VALU op every 4 cycles (MI355X_MICROARCH.md constants table)
+        # one wave alone issues a dependent VALU op every ~4 cycles (MI355X_MICROARCH.md constants
+        # table; tools/probes/launch_floor.py measures 4.1 cycles per op of a dependent FMA chain)
         valu = {"insts_per_wave": pmc["valu_insts_per_wave"], "waves": pmc["SQ_WAVES"],
                 "issue_frac_of_kernel_time": pmc["valu_insts_per_wave"] * 4 / (kern_ms * 1e-3 * 2.4e9),
-                "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave rate "
-                        "(4 cyc/op, 2.4 GHz), per-wave average over the dynamics and observation waves; the "
-                        "rest is dependency/memory latency"}
+                "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave "
+                        "dependent-op rate (4 cyc/op, 2.4 GHz), per-wave average over the kernel's waves "
+                        "(contacts off: dynamics, observation and prep waves); the rest is dependency/memory "
+                        "latency and the ~2.3 us launch floor of an empty kernel of this grid"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -305,8 +307,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kern_ms, "valu": valu,
                          "algorithmic_bytes_per_env_step": bpe,
-                         "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation waves (lane "
-                                 "mapping), i.e. 128 of 1024 SIMDs; HBM fraction is tiny by construction"},
+                         "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation + 64 prep "
+                                 "waves (lane mapping, contacts off), i.e. 192 of 1024 SIMDs; HBM fraction is "
+                                 "tiny by construction"},
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
             "obstacles": obstacles,
         }
