@@ -1301,18 +1301,26 @@ constexpr int eu_words() {
   return n;
 }
 constexpr int EU_VEC = (eu_words() + 3) / 4;
-__device__ __forceinline__ void euler_factor(const float qpos[13], float L[NV][NV]) {
+// chol(M) (EU = false: qacc_smooth) or chol(M + h diag(damping)) (EU: implicit Euler) at the
+// front steer angles d2, d3
+template <bool EU>
+__device__ __forceinline__ void mass_factor(float d2, float d3, float L[NV][NV]) {
   float sa[2][3];
 #pragma unroll
   for (int s = 0; s < 2; s++) {
     float c, sn;
-    fsincos(qpos[W_STEER_QPOS[2 + s]], sn, c);
+    fsincos(s == 0 ? d2 : d3, sn, c);
     rot_axis(sa[s], S_AXIS[s], W_SPIN_AXIS[2 + s], c, sn);
   }
   build_M(L, sa);
+  if constexpr (EU) {
 #pragma unroll
-  for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
+    for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
+  }
   chol_sp<LANE_K(0)>(L);
+}
+__device__ __forceinline__ void euler_factor(const float qpos[13], float L[NV][NV]) {
+  mass_factor<true>(qpos[W_STEER_QPOS[2]], qpos[W_STEER_QPOS[3]], L);
 }
 __device__ __forceinline__ void eu_put(float* x, int lane, const float L[NV][NV]) {
   float w[4 * EU_VEC];
@@ -1375,10 +1383,12 @@ __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV],
 }
 
 // forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
-template <int NC, bool XEU = false>  // NC = 1: compiled for contacts off (MJCF <flag contact="disable"/>)
+// XEU / XM: the Euler / mass-matrix factor comes from another wave (eh / mh), see step_split
+template <int NC, bool XEU = false, bool XM = false>  // NC = 1: compiled for contacts off (<flag contact="disable"/>)
 __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
                                          const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
-                                         const ScalRows& sr, StepResult& out, EuHand eh = EuHand{}) {
+                                         const ScalRows& sr, StepResult& out, EuHand eh = EuHand{},
+                                         EuHand mh = EuHand{}) {
   float(&sa)[2][3] = P.sa;
   float(&cyl)[2][3] = P.cyl;
   Solver& sv = P.sv;
@@ -1401,11 +1411,16 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
   }
   // qacc_smooth = M^-1 fs
   float L[NV][NV];
+  if constexpr (XM) {  // factored by the observation wave (same steer angles)
+    while (__hip_atomic_load(mh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+    eu_get(mh.x, mh.lane, L);
+  } else {
 #pragma unroll
-  for (int i = 0; i < NV; i++)
+    for (int i = 0; i < NV; i++)
 #pragma unroll
-    for (int j = 0; j < NV; j++) L[i][j] = sv.M[i][j];
-  chol_sp<LANE_K(0)>(L);
+      for (int j = 0; j < NV; j++) L[i][j] = sv.M[i][j];
+    chol_sp<LANE_K(0)>(L);
+  }
 #pragma unroll
   for (int i = 0; i < NV; i++) sv.a0[i] = sv.fs[i];
   chol_sp_solve<LANE_K(0)>(L, sv.a0);
@@ -2074,8 +2089,13 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 #ifndef AK_PREP_RAYS
 #define AK_PREP_RAYS 40  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
 #endif
-static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU), "prep rays and the Euler factor need the prep wave");
+#ifndef AK_XM
+#define AK_XM 1  // with AK_XCH: the observation wave factors M (qacc_smooth) before its observation
+#endif
+static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU && !AK_XM), "the hand-overs need the prep wave's exchange");
 constexpr int XEU_OFF = (XCH_WORDS + 1) * 64;  // float offset of the Euler factor words in xch
+constexpr int XM_OFF = XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0);  // ... and of the mass-matrix factor
+constexpr int XCH_FLOATS = XM_OFF + (AK_XM ? 4 * EU_VEC * 64 : 0);
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
@@ -2092,7 +2112,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
   if constexpr (AK_XCH) {
-    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; }
+    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; }
     __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
   if (valid) {
@@ -2138,7 +2158,8 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   }
   if (valid) {
     StepResult res;
-    dyn_post<NC, AK_XEU != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res, EuHand{xch + XEU_OFF, xflag + 2, lane});
+    dyn_post<NC, AK_XEU != 0, AK_XM != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
+                                          EuHand{xch + XEU_OFF, xflag + 2, lane}, EuHand{xch + XM_OFF, xflag + 3, lane});
     if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
       bad_state = redo = true;
       reset_to_qpos0(qpos, qvel, warm, ctrl);
@@ -2169,7 +2190,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   STAMP(10);
 }
 
-__device__ __forceinline__ void step_obs_wave(const Args& A, const float* xch, int* xflag, const uint8_t* sh_bad,
+__device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad,
                                               uint8_t* sh_reset, int lane, int e, bool valid, int slot, int npair) {
   STAMP_SCOPE
   if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
@@ -2200,6 +2221,16 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, const float* xch, i
     for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
 #pragma unroll
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
+  }
+  if constexpr (AK_XM) {  // chol(M) for the dynamics wave's qacc_smooth, at qpos0 for a reset state
+    if (valid) {
+      float L[NV][NV];
+      mass_factor<false>(bad_state ? QPOS0[W_STEER_QPOS[2]] : qpos[W_STEER_QPOS[2]],
+                         bad_state ? QPOS0[W_STEER_QPOS[3]] : qpos[W_STEER_QPOS[3]], L);
+      eu_put(xch + XM_OFF, lane, L);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   const uint32_t nstep = step + 1;
   const bool trunc = nstep >= (uint32_t)A.prm.max_episode_steps;
@@ -2361,8 +2392,8 @@ template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
   static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ __attribute__((aligned(16))) float xch[AK_XCH ? XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0) : 1];
-  __shared__ int xflag[3];
+  __shared__ __attribute__((aligned(16))) float xch[AK_XCH ? XCH_FLOATS : 1];
+  __shared__ int xflag[4];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
