@@ -272,6 +272,13 @@ def test_bad_state_resets(blob, variant, contacts):
     st = sim.state.clone()
     st[13, :8] = float("nan")          # bad qvel
     st[0, 8:16] = 3e10                  # bad qpos
+    # steer angles away from qpos0 on the bad envs (and some good ones): a reset state is observed
+    # and integrated from qpos0 whatever its loaded angles. (The contacts-off kernel's helper waves
+    # also factor M / M + hB at qpos0 for it; from a resting qpos0 the steer-dependent entries --
+    # wheel spin inertia times the spin axis -- move the result by less than the tolerances, as a
+    # negative control with factors taken at the loaded angles showed, tools/negctl.sh)
+    st[9, :24] = 0.4
+    st[11, :24] = -0.3
     sim.set_state(st)
     acts = sim.random_actions(3, seed=seed)
     teacher_forced(sim, fresh_oracle(blob), acts, 3, 2 | (1 if contacts else 0), seed)
