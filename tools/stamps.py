@@ -36,7 +36,8 @@ QUAD_PHASES = [(0, 1, "load+controller"), (1, 2, "kinematics"), (2, 3, "M/bias/a
 
 
 def main():
-    quad = len(sys.argv) > 1 and sys.argv[1] == "quad"
+    quad = len(sys.argv) > 1 and sys.argv[1] in ("quad", "obst")
+    obst = len(sys.argv) > 1 and sys.argv[1] == "obst"
     phases = QUAD_PHASES if quad else PHASES
     L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", os.environ.get("DIAG_LIB", "libackphys_stamps.so")))
     P = C.c_void_p
@@ -45,7 +46,9 @@ def main():
     L.ackphys_reset.argtypes = [P, P, C.c_uint64, P, P, P]
     L.ackphys_random_actions.argtypes = [P, P, C.c_int, C.c_uint64, C.c_uint32, P]
     L.ackphys_diag_set_stamps.argtypes = [P]
-    blob = open(os.path.join(REPO, "mujoco_playground_amd", "model", "assets", "ackermann_robot_v2.apm"), "rb").read()
+    sys.path.insert(0, REPO)
+    from mujoco_playground_amd import _lib
+    blob = _lib.load_blob("obstacles" if obst else "flat")
     n = 4096
     dev = torch.device("cuda:0")
     ctx = P()
