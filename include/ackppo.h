@@ -68,6 +68,16 @@ int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env
                uint32_t step, int deterministic, float* obs_rows, float* action, float* env_action,
                float* log_prob, float* value, void* stream);
 
+/* ackppo_act for rollout step t + 1 fused with the TimeLimit bootstrap of step t (saves the
+ * ackppo_bootstrap launch on every step but the last): the same outputs as ackppo_act, plus
+ * exactly ackppo_bootstrap's reward_out / done_out for the previous step's terminal_obs_soa,
+ * reward, term, trunc (read before this launch overwrites nothing they hold). */
+int ackppo_act_boot(const float* params, const float* obs_soa, int n_env, int64_t env_offset, uint64_t seed,
+                    uint32_t step, int deterministic, float* obs_rows, float* action, float* env_action,
+                    float* log_prob, float* value, const float* terminal_obs_soa, const float* reward,
+                    const uint8_t* term, const uint8_t* trunc, float gamma, float* reward_out, float* done_out,
+                    void* stream);
+
 /* value [n] = critic(obs_soa) (SB3 policy.predict_values; last_values of a rollout). */
 int ackppo_value(const float* params, const float* obs_soa, int n_env, float* value, void* stream);
 

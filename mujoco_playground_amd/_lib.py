@@ -88,7 +88,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
 EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
-PPO_EXPORTS = ["ackppo_act", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
+PPO_EXPORTS = ["ackppo_act", "ackppo_act_boot", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
                "ackppo_adv_moments", "ackppo_adv_finalize", "ackppo_grad",
                "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_permutation",
                "ackppo_last_error"]
@@ -139,6 +139,7 @@ def ppo_lib():
         raise ExtensionMissing(f"cannot load {PPO_LIB_PATH}: {e}") from e
     P, i32, i64, u32, u64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
     L.ackppo_act.argtypes = [P, P, i32, i64, u64, u32, i32, P, P, P, P, P, P]
+    L.ackppo_act_boot.argtypes = [P, P, i32, i64, u64, u32, i32, P, P, P, P, P, P, P, P, P, f32, P, P, P]
     L.ackppo_value.argtypes = [P, P, i32, P, P]
     L.ackppo_bootstrap.argtypes = [P, P, P, P, P, i32, f32, P, P, P]
     L.ackppo_gae.argtypes = [P, P, P, P, P, i32, i32, f32, f32, P, P, P]

@@ -155,6 +155,14 @@ struct ActArgs {
   float* env_action;
   float* log_prob;
   float* value;
+  // previous rollout step's TimeLimit bootstrap (ackppo_act_boot; tobs == nullptr: none)
+  const float* tobs;
+  const float* reward;
+  const uint8_t* term;
+  const uint8_t* trunc;
+  float gamma;
+  float* reward_out;
+  float* done_out;
 };
 
 // Policy tile: 64 envs (lane = env) x PT_WAVES waves. The whole parameter vector is staged in
@@ -879,27 +887,10 @@ constexpr int AE = 16;  // envs per workgroup
 constexpr int A_X = W_TOTAL, A_H1 = A_X + 80 * AE, A_H2 = A_H1 + 2 * H * AE, A_TOTAL = A_H2 + 2 * H * AE;
 constexpr size_t ACT_LDS = (size_t)A_TOTAL * sizeof(float);
 
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(ActArgs A) {
-  extern __shared__ float tl[];
-  float* w = tl;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+// layers 1-2 of both nets and the three heads for the 16 envs of X (already in LDS): returns, in
+// wave 0, lane (env li, output lk) = mu0 / mu1 / value
+__device__ __forceinline__ float act_forward(float* tl, const float* w, int wave, int lane) {
   const int li = lane & 15, lk = lane >> 4;
-  const int e0 = blockIdx.x * AE, nv = min(AE, A.n - e0);
-  stage_grad_weights(A.params, w);
-  {  // X [k][env] from the SoA observation (row 79 and padding envs zero)
-    const int e = tid & 15;
-#pragma unroll
-    for (int k = tid >> 4; k < 80; k += 16)
-      tl[A_X + k * AE + e] = (k < NOBS && e < nv) ? A.obs[(size_t)k * A.n + e0 + e] : 0.0f;
-  }
-  __syncthreads();
-  if (A.obs_rows) {  // rollout-buffer rows [env][79]: one contiguous block of nv * 79 words
-    for (int i = tid; i < nv * NOBS; i += GRAD_THREADS) {
-      const int e = i / NOBS, k = i - e * NOBS;
-      A.obs_rows[(size_t)e0 * NOBS + i] = tl[A_X + k * AE + e];
-    }
-  }
   const int nid = wave >> 1, ub0 = 32 * (wave & 1);
   {  // layer 1: [128 x 16] = W1T^T [128 x 80] . X [80 x 16]
     f4v acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -939,16 +930,64 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
     }
   }
   __syncthreads();
-  if (wave != 0) return;
   // heads: lane (env li, output lk): 0 mu0, 1 mu1 (actor H2 rows 0-63), 2 value (critic rows 64-127)
   float v = 0.0f;
-  {
+  if (wave == 0) {
     const int wo = lk == 0 ? W_AW : (lk == 1 ? W_AW + H : W_CW);
     const float* h2 = tl + A_H2 + (lk == 2 ? H * AE : 0);
 #pragma unroll 8
     for (int j = 0; j < H; j++) v = fmaf(w[wo + j], h2[j * AE + li], v);
     v += lk == 0 ? w[W_AB] : (lk == 1 ? w[W_AB + 1] : w[W_CB]);
   }
+  return v;
+}
+__device__ __forceinline__ void act_load_x(float* tl, const float* soa, int n, int e0, int nv, int tid) {
+  // X [k][env] from an SoA observation (row 79 and padding envs zero)
+  const int e = tid & 15;
+#pragma unroll
+  for (int k = tid >> 4; k < 80; k += 16) tl[A_X + k * AE + e] = (k < NOBS && e < nv) ? soa[(size_t)k * n + e0 + e] : 0.0f;
+}
+
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(ActArgs A) {
+  extern __shared__ float tl[];
+  float* w = tl;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  const int e0 = blockIdx.x * AE, nv = min(AE, A.n - e0);
+  stage_grad_weights(A.params, w);
+  if (A.tobs) {
+    // the previous step's TimeLimit bootstrap (ackppo_bootstrap's semantics): the critic on the
+    // terminal observations, only in workgroups holding a truncated-not-terminated env (rare)
+    const int eb = e0 + (tid & 15);
+    const bool mine = tid < AE && (tid & 15) < nv;
+    const bool te = mine && A.term[eb] != 0, tr = mine && A.trunc[eb] != 0;
+    const bool boot = tr && !te;
+    float vb = 0.0f;
+    if (__syncthreads_or(boot)) {
+      act_load_x(tl, A.tobs, A.n, e0, nv, tid);
+      __syncthreads();
+      const float v = act_forward(tl, w, wave, lane);
+      vb = __shfl(v, (tid & 15) + 32, 64);  // wave 0: value of env tid & 15
+      __syncthreads();                      // X is reloaded below
+    }
+    if (mine) {
+      float r = A.reward[eb];
+      if (boot) r += A.gamma * vb;
+      A.reward_out[eb] = r;
+      A.done_out[eb] = (te || tr) ? 1.0f : 0.0f;
+    }
+  }
+  act_load_x(tl, A.obs, A.n, e0, nv, tid);
+  __syncthreads();
+  if (A.obs_rows) {  // rollout-buffer rows [env][79]: one contiguous block of nv * 79 words
+    for (int i = tid; i < nv * NOBS; i += GRAD_THREADS) {
+      const int e = i / NOBS, k = i - e * NOBS;
+      A.obs_rows[(size_t)e0 * NOBS + i] = tl[A_X + k * AE + e];
+    }
+  }
+  const float v = act_forward(tl, w, wave, lane);
+  if (wave != 0) return;
   const float mu1 = __shfl(v, li + 16, 64), val = __shfl(v, li + 32, 64);
   if (lk != 0 || li >= nv) return;
   const int e = e0 + li;
@@ -1153,11 +1192,29 @@ int ackppo_act(const float* params, const float* obs_soa, int n_env, int64_t env
                void* stream) {
   if (!params || !obs_soa || !env_action || n_env < 0) return fail(ACKPPO_EINVAL, "ackppo_act: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
-  ActArgs A{params, obs_soa, n_env, env_offset, seed, step, deterministic, obs_rows, action, env_action, log_prob, value};
+  ActArgs A{params, obs_soa, n_env, env_offset, seed, step, deterministic, obs_rows, action, env_action, log_prob, value,
+            nullptr, nullptr, nullptr, nullptr, 0.0f, nullptr, nullptr};
   if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_act: cannot reserve the policy LDS tile");
   hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + AE - 1) / AE), dim3(GRAD_THREADS), ACT_LDS, (hipStream_t)stream,
                      A);
   return launched("ackppo_act");
+}
+
+int ackppo_act_boot(const float* params, const float* obs_soa, int n_env, int64_t env_offset, uint64_t seed,
+                    uint32_t step, int deterministic, float* obs_rows, float* action, float* env_action,
+                    float* log_prob, float* value, const float* terminal_obs_soa, const float* reward,
+                    const uint8_t* term, const uint8_t* trunc, float gamma, float* reward_out, float* done_out,
+                    void* stream) {
+  if (!params || !obs_soa || !env_action || n_env < 0 || !terminal_obs_soa || !reward || !term || !trunc ||
+      !reward_out || !done_out)
+    return fail(ACKPPO_EINVAL, "ackppo_act_boot: bad arguments");
+  if (n_env == 0) return ACKPPO_OK;
+  ActArgs A{params,  obs_soa,          n_env,  env_offset, seed, step,  deterministic, obs_rows,   action, env_action,
+            log_prob, value, terminal_obs_soa, reward, term,       trunc, gamma, reward_out,    done_out};
+  if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_act_boot: cannot reserve the policy LDS tile");
+  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + AE - 1) / AE), dim3(GRAD_THREADS), ACT_LDS, (hipStream_t)stream,
+                     A);
+  return launched("ackppo_act_boot");
 }
 
 int ackppo_value(const float* params, const float* obs_soa, int n_env, float* value, void* stream) {

@@ -212,17 +212,27 @@ class PPO:
         if not self._last_obs_ready:
             self.env.reset()
             self._last_obs_ready = True
+        # episode starts: step t's done flags are step t + 1's starts, so the bootstrap writes them
+        # straight into buf_start[t + 1] (the last step's into last_dones): one copy per rollout
+        self.buf_start[0].copy_(self.last_dones)
+        # The TimeLimit bootstrap of step t rides in step t + 1's act launch (ackppo_act_boot); the
+        # last step's is its own launch.
         for t in range(self.n_steps):
-            self.buf_start[t].copy_(self.last_dones)
-            _lib.ppo_check(L.ackppo_act(_ptr(self.params), _ptr(sim.obs_soa), N, self.env_offset, self.seed,
-                                        self._rollout_step, 0, _ptr(self.buf_obs[t * N]),
-                                        _ptr(self.buf_act[t * N]), _ptr(self.env_action), _ptr(self.buf_logp[t]),
-                                        _ptr(self.buf_val[t]), s), "ackppo_act")
+            out = (_ptr(self.params), _ptr(sim.obs_soa), N, self.env_offset, self.seed, self._rollout_step, 0,
+                   _ptr(self.buf_obs[t * N]), _ptr(self.buf_act[t * N]), _ptr(self.env_action),
+                   _ptr(self.buf_logp[t]), _ptr(self.buf_val[t]))
+            if t == 0:
+                _lib.ppo_check(L.ackppo_act(*out, s), "ackppo_act")
+            else:
+                _lib.ppo_check(L.ackppo_act_boot(*out, _ptr(sim.terminal_obs_soa), _ptr(sim.reward), _ptr(sim.term),
+                                                 _ptr(sim.trunc), self.gamma, _ptr(self.buf_rew[t - 1]),
+                                                 _ptr(self.buf_start[t]), s), "ackppo_act_boot")
             sim.step(self.env_action, autoreset=True, want_info=False, want_terminal=True, track_episodes=True)
-            _lib.ppo_check(L.ackppo_bootstrap(_ptr(self.params), _ptr(sim.terminal_obs_soa), _ptr(sim.reward),
-                                              _ptr(sim.term), _ptr(sim.trunc), N, self.gamma, _ptr(self.buf_rew[t]),
-                                              _ptr(self.last_dones), s), "ackppo_bootstrap")
             self._rollout_step += 1
+        _lib.ppo_check(L.ackppo_bootstrap(_ptr(self.params), _ptr(sim.terminal_obs_soa), _ptr(sim.reward),
+                                          _ptr(sim.term), _ptr(sim.trunc), N, self.gamma,
+                                          _ptr(self.buf_rew[self.n_steps - 1]), _ptr(self.last_dones), s),
+                       "ackppo_bootstrap")
         self.num_timesteps += self.n_steps * N * self.world
         _lib.ppo_check(L.ackppo_value(_ptr(self.params), _ptr(sim.obs_soa), N, _ptr(self.last_values), s),
                        "ackppo_value")

@@ -67,6 +67,41 @@ def test_act_matches_oracle():
     np.testing.assert_allclose(vv.cpu().numpy(), ov, rtol=1e-5, atol=2e-5)
 
 
+def test_act_boot_equals_act_plus_bootstrap():
+    """ackppo_act_boot = ackppo_act (bit-identical: the same kernel path for the policy outputs) and
+    ackppo_bootstrap's rewards / done flags for the previous step (the oracle's bootstrap); the
+    truncations sit in a few 16-env workgroups only, so both the critic branch and its skip run."""
+    flat, p = params_dev(3)
+    n = 301
+    rng = np.random.default_rng(5)
+    obs = rng.normal(0, 2, (n, 79)).astype(np.float32)
+    tobs = rng.normal(0, 1, (n, 79)).astype(np.float32)
+    rew = rng.normal(0, 1, n).astype(np.float32)
+    term = np.zeros(n, np.uint8)
+    trunc = np.zeros(n, np.uint8)
+    trunc[[3, 17, 18, 200, 300]] = 1
+    term[[17, 40]] = 1                     # env 17: terminated and truncated -> no bootstrap
+    t = lambda a: torch.tensor(a, device=DEV)
+    soa, tsoa = t(obs.T.copy()), t(tobs.T.copy())
+
+    def outs():
+        return [torch.zeros(n, 79, device=DEV), torch.zeros(n, 2, device=DEV), torch.zeros(n, 2, device=DEV),
+                torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)]
+    a1, a2 = outs(), outs()
+    assert L().ackppo_act(P(p), P(soa), n, 7, 99, 3, 0, *[P(x) for x in a1], S()) == 0
+    ro, do = torch.full((n,), -7.0, device=DEV), torch.full((n,), -7.0, device=DEV)
+    assert L().ackppo_act_boot(P(p), P(soa), n, 7, 99, 3, 0, *[P(x) for x in a2], P(tsoa), P(t(rew)), P(t(term)),
+                               P(t(trunc)), 0.99, P(ro), P(do), S()) == 0
+    torch.cuda.synchronize()
+    for x, y in zip(a1, a2):
+        assert torch.equal(x, y)
+    r_ref, d_ref = po.bootstrap(flat.astype(np.float32).astype(np.float64), tobs, rew, term, trunc, 0.99)
+    np.testing.assert_allclose(ro.cpu().numpy(), r_ref, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(do.cpu().numpy(), d_ref)
+    boot = (trunc == 1) & (term == 0)
+    assert np.array_equal(ro.cpu().numpy()[~boot], rew[~boot]) and not np.allclose(r_ref[boot], rew[boot])
+
+
 def test_checkpoint_policy_on_gpu():
     d = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "ppo_policy.npz"))
     for k in (10000, 20000, 30000):
