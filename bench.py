@@ -236,6 +236,25 @@ def load_pmc(kern_name: str, contacts: bool):
         return None
 
 
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md constants table (spec)
+
+
+def oracle_flops(config_key: str, rate: float):
+    """The reference algorithm's FLOPs per env-step for this workload, counted in the CPU oracle
+    (tools/count_flops.py -> profiles/oracle_flops.json), and the effective FP32 rate
+    they imply at `rate` env-steps/s; None if that profile is absent."""
+    try:
+        with open(os.path.join(HERE, "profiles", "oracle_flops.json")) as f:
+            c = json.load(f)["configs"][config_key]
+    except (OSError, ValueError, KeyError):
+        return None
+    eff = c["flops_per_env_step"] * rate / 1e12
+    return {"oracle_flops_per_env_step": c["flops_per_env_step"], "effective_tflops": eff,
+            "fp32_vector_peak_tflops": FP32_VECTOR_PEAK_TFLOPS, "frac": eff / FP32_VECTOR_PEAK_TFLOPS,
+            "note": "FLOPs of the reference's algorithm (f64 oracle, + - * / sqrt) per env-step x env-steps/s; "
+                    "the kernels execute fewer (structured factorisations, floor-only rays, predicted pieces)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,7 +282,9 @@ def main():
         _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant)
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
                      "kernel_ms": km2,
-                     "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup}
+                     "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup,
+                     "flops": oracle_flops("configs[1] contacts off" if contacts else "configs[2] contacts on",
+                                           total_envs * a.steps / el2)}
     ppo = None if a.no_ppo else run_ppo(a.envs, rank, world, device)
     obstacles = None
     if not a.no_obstacles:
@@ -273,6 +294,7 @@ def main():
                      "value": total_envs * a.steps / el3, "unit": "env-steps/s", "ms_per_step": el3 * 1e3 / a.steps,
                      "kernel": "ackphys_step_obst_kernel", "kernel_ms": km3, "episodes": rets3,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS),
+                     "flops": oracle_flops("configs[4] obstacle scene, contacts on", total_envs * a.steps / el3),
                      "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
     parity = base = None
     if rank == 0 and not a.no_cpu:
@@ -306,6 +328,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kern, "kernel_ms": kern_ms, "valu": valu,
+                         "flops": oracle_flops("configs[2] contacts on" if contacts else "configs[1] contacts off",
+                                               value),
                          "algorithmic_bytes_per_env_step": bpe,
                          "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation + 64 prep "
                                  "waves (lane mapping, contacts off), i.e. 192 of 1024 SIMDs; HBM fraction is "

@@ -33,6 +33,13 @@
 #include "../include/ackphys_model.h"
 #include "ackphys_oracle.h"
 
+/* stage markers for the FLOP-counting build (oracle/flops/fd.hpp, `make flops`); no-ops here.
+ * 1 controller, 2 kinematics, 3 mass matrix, 4 collision, 5 sensors (rays), 6 velocity/bias/
+ * actuation, 7 qacc_smooth, 8 constraint rows, 9 Newton solver, 10 Euler, 11 obs/reward, 12 reset */
+#ifndef OR_STAGE
+#define OR_STAGE(k) ((void)0)
+#endif
+
 #define mjMINVAL 1e-15
 #define mjMINIMP 0.0001
 #define mjMAXIMP 0.9999
@@ -1500,16 +1507,22 @@ static void reset_data(const or_ctx* c, or_data* d) {
 
 static void forward(const or_ctx* c, or_data* d, uint32_t flags) {
   const apm_model_t* m = c->m;
+  OR_STAGE(2);
   kinematics(c, d);
   com_pos(c, d);
+  OR_STAGE(3);
   crb(c, d);
+  OR_STAGE(4);
   if (flags & FLAG_CONTACTS) collision(c, d);
   else d->ncon = 0;
+  OR_STAGE(5);
   sensors(c, d); /* positional + velocity sensors (joint sensors read qpos/qvel directly) */
+  OR_STAGE(6);
   com_vel(c, d);
   rne(c, d);
   passive(c, d);
   actuation(c, d);
+  OR_STAGE(7);
   int nv = m->nv;
   for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
   double L[APM_MAXDOF * APM_MAXDOF];
@@ -1517,8 +1530,11 @@ static void forward(const or_ctx* c, or_data* d, uint32_t flags) {
   cholesky(L, nv);
   memcpy(d->qacc_smooth, d->qfrc_smooth, sizeof(double) * nv);
   chol_solve(L, nv, d->qacc_smooth);
+  OR_STAGE(8);
   make_constraint(c, d);
+  OR_STAGE(9);
   solve_newton(c, d);
+  OR_STAGE(0);
 }
 
 static void integrate_pos(const or_ctx* c, double* qpos, const double* qvel, double h) {
@@ -1578,7 +1594,9 @@ static void mj_step(const or_ctx* c, or_data* d, uint32_t flags) {
     reset_data(c, d);
     forward(c, d, flags);
   }
+  OR_STAGE(10);
   euler(c, d);
+  OR_STAGE(0);
 }
 
 /* ------------------------------------------------------------------ env glue */
@@ -1704,7 +1722,9 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
                      double* terminal_obs, double info[4]) {
   load_state(c, d, st);
   double ctrl[3];
+  OR_STAGE(1);
   or_controller2(action, c->max_lin, c->max_ang, ctrl);
+  OR_STAGE(0);
   d->bad_ctrl = 0;
   for (int k = 0; k < 3; k++)
     if (is_bad(ctrl[k])) d->bad_ctrl = 1;
@@ -1720,7 +1740,9 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
   }
   int t;
   double inf3[3];
+  OR_STAGE(11);
   observe(c, d, st + ST_GOAL, st + ST_REF, obs, reward, &t, inf3);
+  OR_STAGE(0);
   store_state(c, d, st);
   st[ST_STEP] += 1;
   int tr = st[ST_STEP] >= c->max_steps;
@@ -1729,7 +1751,9 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
   if (info) { info[0] = inf3[0]; info[1] = inf3[1]; info[2] = inf3[2]; info[3] = d->bad_state; }
   if ((flags & FLAG_AUTORESET) && (t || tr)) {
     if (terminal_obs) memcpy(terminal_obs, obs, sizeof(double) * NOBS);
+    OR_STAGE(12);
     env_reset(c, d, st, env, seed, obs);
+    OR_STAGE(0);
   }
 }
 

@@ -208,3 +208,54 @@ def test_step_cpu_twin_matches_row_oracle(blob):
         np.testing.assert_array_equal(tobs.T[done], to[done].astype(np.float32))
     assert np.all(ep[3] == 1)    # one truncated episode of 12 steps each in 20 steps
     np.testing.assert_array_equal(ep[1], np.full(n, 8, np.float32))
+
+
+def test_flop_counting_build_matches_the_oracle(tmp_path):
+    """The FLOP-counting oracle build (oracle/flops/fd.hpp, `make -C oracle flops`) computes the same
+    states as the plain oracle (the counting double only observes) and attributes its operations to
+    the stages the bench reports (tools/count_flops.py -> profiles/oracle_flops.json)."""
+    import ctypes as C
+    import os
+    import subprocess
+
+    import numpy as np
+
+    from mujoco_playground_amd import _lib
+    from oracle import oracle as orc
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-C", os.path.join(repo, "oracle"), "flops"], check=True, capture_output=True)
+    F = C.CDLL(os.path.join(repo, "oracle", "build", "libackphys_oracle_flops.so"))
+    R = orc.lib()
+    P, i32, u32, u64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64
+    ULL = C.c_ulonglong * 16
+    for L in (F, R):
+        L.or_create.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(P)]
+        L.ackphys_reset_cpu.argtypes = [P, i32, P, u64, P, P]
+        L.ackphys_step_cpu.argtypes = [P, i32] + [P] * 9 + [u32, u64, i32]
+    F.or_flops_read.argtypes = [ULL, ULL, i32]
+    blob = _lib.load_blob("flat")
+    n, ptr = 16, (lambda x: x.ctypes.data_as(P))
+    out = []
+    for L in (F, R):
+        ctx = P()
+        assert L.or_create(blob, len(blob), C.byref(ctx)) == 0
+        st, obs = np.zeros((44, n), np.float32), np.zeros((79, n), np.float32)
+        rew, term, trunc = np.zeros(n, np.float32), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+        assert L.ackphys_reset_cpu(ctx, n, None, 3, ptr(st), ptr(obs)) == 0
+        if L is F:
+            F.or_flops_reset()
+        rng = np.random.default_rng(1)
+        for _ in range(5):
+            act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+            assert L.ackphys_step_cpu(ctx, n, ptr(act), ptr(st), ptr(obs), ptr(rew), ptr(term), ptr(trunc), None,
+                                      None, None, 3, 3, 1) == 0
+        out.append((st.copy(), obs.copy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    fl, tr = ULL(), ULL()
+    F.or_flops_read(fl, tr, 16)
+    per = np.array(fl[:13], dtype=float) / (n * 5)
+    # controller, kinematics, mass matrix, collision, rays, bias, qacc_smooth, rows, Newton, Euler
+    assert (per[[1, 2, 3, 4, 5, 6, 7, 8, 9, 10]] > 0).all()
+    assert 2e4 < per.sum() < 2e5
