@@ -26,10 +26,10 @@ from mujoco_playground_amd import _lib  # noqa: E402  (model blobs only)
 
 STAGES = ["glue", "controller", "kinematics", "mass matrix", "collision", "sensors (rays)", "velocity/bias/actuation",
           "qacc_smooth", "constraint rows", "Newton solver", "Euler", "obs/reward", "reset"]
-CONFIGS = [  # (name, scene, flags, untimed steps from reset, counted steps)
-    ("configs[1] contacts off", "flat", 2, 50, None),
-    ("configs[2] contacts on", "flat", 3, 200, None),
-    ("configs[4] obstacle scene, contacts on", "obstacles", 3, 200, None),
+CONFIGS = [  # (name, scene, flags, untimed steps from reset: bench.py's warm-up / landing settle)
+    ("configs[1] contacts off", "flat", 2, 50),
+    ("configs[2] contacts on", "flat", 3, 200),
+    ("configs[4] obstacle scene, contacts on", "obstacles", 3, 200),
 ]
 
 
@@ -50,7 +50,7 @@ def main():
     n = a.envs
     ptr = lambda x: x.ctypes.data_as(P)
     res = {"note": __doc__.split("\n\n")[1].replace("\n", " "), "envs": n, "configs": {}}
-    for name, scene, flags, warm, _ in CONFIGS:
+    for name, scene, flags, warm in CONFIGS:
         blob = _lib.load_blob(scene)
         ctx = P()
         assert L.or_create(blob, len(blob), C.byref(ctx)) == 0
@@ -60,7 +60,6 @@ def main():
         tobs, info, ep = np.zeros((79, n), np.float32), np.zeros((4, n), np.float32), np.zeros((4, n), np.float32)
         assert L.ackphys_reset_cpu(ctx, n, None, 7, ptr(st), ptr(obs)) == 0
         rng = np.random.default_rng(0)
-        counts = None
         for k in range(warm + a.steps):
             if k == warm:
                 L.or_flops_reset()
