@@ -67,6 +67,19 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
   }
 }
 
+// tanh of the policy's hidden units: Cephes tanhf's form -- |x| < 0.625: x + x^3 P(x^2), else
+// 1 - 2 / (exp(2|x|) + 1) -- with the hardware exp2 / rcp instead of the library's expf and
+// division (a few ulp; the device tanhf is ~2x the instructions). Used by every policy kernel,
+// so the rollout's log_probs and the update's agree exactly.
+__device__ __forceinline__ float ftanh(float x) {
+  const float ax = fabsf(x), z = x * x;
+  const float p = fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z, -5.37397155531e-2f), z,
+                            1.33314422036e-1f), z, -3.33332819422e-1f);
+  const float small = fmaf(x * z, p, x);
+  const float e = __builtin_amdgcn_exp2f(2.88539008178f * ax);  // exp(2|x|); +inf for large |x|
+  const float big = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
+  return ax < 0.625f ? small : big;
+}
 // out[j] = tanh(b[j] + W[j,:] . x) for the 64 units, written to an LDS column (stride cs).
 // W/b addresses are wave-uniform: scalar loads, x stays in VGPRs.
 template <int IN>
@@ -77,7 +90,7 @@ _Pragma(PP_UNROLL_STR)
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < IN; k++) acc = fmaf(W[j * IN + k], x[k], acc);
-    col[j * cs] = tanhf(acc + b[j]);
+    col[j * cs] = ftanh(acc + b[j]);
   }
 }
 
@@ -205,7 +218,7 @@ _Pragma(PP_UNROLL_STR)
       float acc = 0.0f;
 #pragma unroll
       for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
-      L.h1[(hrow + u) * PT_ENVS + lane] = tanhf(acc + b1[u]);
+      L.h1[(hrow + u) * PT_ENVS + lane] = ftanh(acc + b1[u]);
     }
   }
   __syncthreads();
@@ -220,7 +233,7 @@ _Pragma(PP_UNROLL_STR)
       float acc = 0.0f;
 #pragma unroll
       for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
-      L.h2[(hrow + u) * PT_ENVS + lane] = tanhf(acc + b2[u]);
+      L.h2[(hrow + u) * PT_ENVS + lane] = ftanh(acc + b2[u]);
     }
   }
   __syncthreads();
@@ -666,7 +679,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
           const int u = ub0 + 16 * t + 4 * lk + r;
           const float bb = bias[u];
 #pragma unroll
-          for (int j = 0; j < 2; j++) nt[G_H1 + u * GLDP + 16 * j + li] = tanhf(acc[t][j][r] + bb);
+          for (int j = 0; j < 2; j++) nt[G_H1 + u * GLDP + 16 * j + li] = ftanh(acc[t][j][r] + bb);
         }
     }
     __syncthreads();
@@ -696,7 +709,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
           const int u = ub0 + 16 * t + 4 * lk + r;
           const float bb = bias[u];
 #pragma unroll
-          for (int j = 0; j < 2; j++) nt[G_H2 + u * GLDP + 16 * j + li] = tanhf(acc[t][j][r] + bb);
+          for (int j = 0; j < 2; j++) nt[G_H2 + u * GLDP + 16 * j + li] = ftanh(acc[t][j][r] + bb);
         }
     }
     __syncthreads();
@@ -905,8 +918,8 @@ __device__ __forceinline__ float act_forward(float* tl, const float* w, int wave
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int u = ub0 + 4 * lk + r;
-      tl[A_H1 + (nid * H + u) * AE + li] = tanhf(acc0[r] + bias[u]);
-      tl[A_H1 + (nid * H + u + 16) * AE + li] = tanhf(acc1[r] + bias[u + 16]);
+      tl[A_H1 + (nid * H + u) * AE + li] = ftanh(acc0[r] + bias[u]);
+      tl[A_H1 + (nid * H + u + 16) * AE + li] = ftanh(acc1[r] + bias[u + 16]);
     }
   }
   __syncthreads();
@@ -925,8 +938,8 @@ __device__ __forceinline__ float act_forward(float* tl, const float* w, int wave
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int u = ub0 + 4 * lk + r;
-      tl[A_H2 + (nid * H + u) * AE + li] = tanhf(acc0[r] + bias[u]);
-      tl[A_H2 + (nid * H + u + 16) * AE + li] = tanhf(acc1[r] + bias[u + 16]);
+      tl[A_H2 + (nid * H + u) * AE + li] = ftanh(acc0[r] + bias[u]);
+      tl[A_H2 + (nid * H + u + 16) * AE + li] = ftanh(acc1[r] + bias[u + 16]);
     }
   }
   __syncthreads();
