@@ -133,8 +133,8 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
 int ackppo_grad_blocks(int batch);
 
 /* grad [NPARAM] = sum of nblk partial rows (grad is overwritten); d(-ent_coef * entropy)/d log_std = -ent_coef added;
- * loss [8] = column sums of loss_partial. grad_partial is CONSUMED: its first min(nblk, 16) rows are
- * overwritten with row-group sums (no library-owned scratch; the next ackppo_grad rewrites every row). */
+ * loss [8] = column sums of loss_partial. grad_partial is CONSUMED: the library may overwrite its rows with
+ * intermediate sums (no library-owned scratch; the next ackppo_grad rewrites every row). */
 int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream);
 

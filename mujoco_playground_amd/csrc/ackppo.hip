@@ -1075,6 +1075,55 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int 
 // (row by belongs to group by alone, and element (by, p) to one thread, which read it first);
 // (2) sums rows 0..RG-1. The caller-owned partial rows are the only buffer, so concurrent
 // learners on other streams or devices share nothing.
+// One-launch reduction (default): a 1024-thread block owns 64 consecutive parameters; its 16
+// waves each sum every 16th partial row of them (coalesced 256-byte row reads, four loads in
+// flight per lane), the 16 sums are combined through LDS; block 0 also reduces the loss rows.
+// It replaced the two-launch form below (row groups in place, then the group sums).
+#ifndef AK_PPO_REDUCE1
+#define AK_PPO_REDUCE1 1
+#endif
+constexpr int R1_P = 64, R1_G = 16;
+extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce1_kernel(const float* gpart, int nblk,
+                                                                        const float* lpart, float ent_coef,
+                                                                        float* grad, float* loss, int accumulate) {
+  __shared__ float red[R1_G][R1_P + 1];
+  __shared__ float lred[256];
+  const int tid = threadIdx.x, pl = tid & (R1_P - 1), g = tid / R1_P;
+  const int pidx = blockIdx.x * R1_P + pl;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (pidx < P) {
+    int b = g;
+    for (; b + 3 * R1_G < nblk; b += 4 * R1_G) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] += gpart[(size_t)(b + i * R1_G) * P + pidx];
+    }
+    for (; b < nblk; b += R1_G) acc[0] += gpart[(size_t)b * P + pidx];
+  }
+  red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (tid < R1_P && pidx < P) {
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < R1_G; k++) s += red[k][tid];
+    if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
+    grad[pidx] = s;
+  }
+  if (blockIdx.x == 0) {  // loss rows: as ackppo_reduce_kernel, on the block's first 256 threads
+    static_assert(ACKPPO_NLOSS == 8, "loss row layout");
+    const int slot = tid & 7, grp = tid >> 3;
+    float s = 0.0f;
+    if (tid < 256)
+      for (int b = grp; b < nblk; b += 32) s += lpart[(size_t)b * ACKPPO_NLOSS + slot];
+    if (tid < 256) lred[tid] = s;
+    __syncthreads();
+    for (int o = 128; o >= 8; o >>= 1) {
+      if (tid < o) lred[tid] += lred[tid + o];
+      __syncthreads();
+    }
+    if (tid < ACKPPO_NLOSS) loss[tid] = (accumulate ? loss[tid] : 0.0f) + lred[tid];
+  }
+}
+
 constexpr int REDUCE_RG = 16;
 extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(float* gpart, int nblk) {
   const int pidx = blockIdx.x * 256 + threadIdx.x;
@@ -1344,6 +1393,11 @@ int ackppo_grad_blocks(int batch) {
 namespace {
 int reduce_launch(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, int accumulate, void* stream) {
+  if (AK_PPO_REDUCE1) {
+    hipLaunchKernelGGL(ackppo_reduce1_kernel, dim3((P + R1_P - 1) / R1_P), dim3(R1_P * R1_G), 0, (hipStream_t)stream,
+                       grad_partial, nblk, loss_partial, ent_coef, grad, loss, accumulate);
+    return launched("ackppo_reduce");
+  }
   const int rg = nblk < REDUCE_RG ? nblk : REDUCE_RG;
   hipLaunchKernelGGL(ackppo_reduce_rows_kernel, dim3((P + 255) / 256, rg), dim3(256), 0, (hipStream_t)stream,
                      grad_partial, nblk);
