@@ -1167,29 +1167,33 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* params, const float* grad, float* m,
-                                                                     float* v, float scale, float max_norm, float b1,
-                                                                     float b2, float eps, float step_size,
-                                                                     float bc2_sqrt, float* norm_out) {
-  __shared__ float red[256];
+#ifndef ADAM_THREADS
+#define ADAM_THREADS 1024  // 19 blocks; each forms the norm with 18 loads per thread (256: 73); ~4.7 vs 4.8 us
+#endif
+extern "C" __global__ void __launch_bounds__(ADAM_THREADS) ackppo_adam_kernel(float* params, const float* grad,
+                                                                              float* m, float* v, float scale,
+                                                                              float max_norm, float b1, float b2,
+                                                                              float eps, float step_size,
+                                                                              float bc2_sqrt, float* norm_out) {
+  __shared__ float red[ADAM_THREADS];
   const int tid = threadIdx.x;
   // every block forms the global norm itself (75 KB from L2) instead of a second launch
   float ss = 0.0f;
 #pragma unroll 8
-  for (int i = tid; i < P; i += 256) {
+  for (int i = tid; i < P; i += ADAM_THREADS) {
     const float gi = grad[i] * scale;
     ss = fmaf(gi, gi, ss);
   }
   red[tid] = ss;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = ADAM_THREADS / 2; o > 0; o >>= 1) {
     if (tid < o) red[tid] += red[tid + o];
     __syncthreads();
   }
   const float norm = sqrtf(red[0]);
   const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
   if (blockIdx.x == 0 && tid == 0 && norm_out) norm_out[0] = norm;
-  const int i = blockIdx.x * 256 + tid;
+  const int i = blockIdx.x * ADAM_THREADS + tid;
   if (i >= P) return;
   const float gi = grad[i] * scale * coef;
   const float mi = m[i] + (1.0f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
@@ -1417,7 +1421,7 @@ int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg
                 float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
                 float* grad_norm_out, void* stream) {
   if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(ACKPPO_EINVAL, "ackppo_adam: bad arguments");
-  hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, params, grad,
+  hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P + ADAM_THREADS - 1) / ADAM_THREADS), dim3(ADAM_THREADS), 0, (hipStream_t)stream, params, grad,
                      exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
                      grad_norm_out);
   return launched("ackppo_adam");
