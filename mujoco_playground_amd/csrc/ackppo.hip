@@ -610,6 +610,22 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   float* w = tl;
   float* nt = tl + G_NET + nid * G_NETSZ;
   const float invB = 1.0f / (float)A.batch;
+  const int ntiles = (A.batch + GT - 1) / GT;
+  // gather of a tile's observation rows: thread t holds 10 words of row (t >> 3). The first
+  // tile's loads are issued before the weight staging, so their latency hides under it.
+  float xg[10];
+  auto gather_load = [&](int tile) __attribute__((always_inline)) {
+    const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
+    const int r = tid >> 3, q = tid & 7;
+    const bool ok = r < nvalid;
+    const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + r] : 0) * NOBS;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int k = q * 10 + i;
+      xg[i] = (ok && k < NOBS) ? row[k] : 0.0f;
+    }
+  };
+  if (blockIdx.x < ntiles) gather_load(blockIdx.x);
   stage_grad_weights(A.params, w);
 
   // MFMA tiles: lane (li, lk) = (lane & 15, lane >> 4). Wave w owns unit tiles ut = 2w, 2w + 1
@@ -631,22 +647,14 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   for (int b = 0; b < PERV; b++) accv[b] = 0.0f;
   float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
 
-  const int ntiles = (A.batch + GT - 1) / GT;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
     __syncthreads();  // previous tile's LDS reads are done (and the weights are staged)
-    {  // gather: thread t copies 10 words of row (t >> 3)
+    if (tile != blockIdx.x) gather_load(tile);
+    {
       const int r = tid >> 3, q = tid & 7;
-      const bool ok = r < nvalid;
-      const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + r] : 0) * NOBS;
-      float v[10];
 #pragma unroll
-      for (int i = 0; i < 10; i++) {
-        const int k = q * 10 + i;
-        v[i] = (ok && k < NOBS) ? row[k] : 0.0f;
-      }
-#pragma unroll
-      for (int i = 0; i < 10; i++) tl[G_X + (q * 10 + i) * GLDP + r] = v[i];
+      for (int i = 0; i < 10; i++) tl[G_X + (q * 10 + i) * GLDP + r] = xg[i];
     }
     __syncthreads();
     PSTAMP(1);
