@@ -625,7 +625,28 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
       xg[i] = (ok && k < NOBS) ? row[k] : 0.0f;
     }
   };
-  if (blockIdx.x < ntiles) gather_load(blockIdx.x);
+  // the heads' per-sample inputs (actor lanes: action, old log-prob, advantage; critic lanes:
+  // return), loaded with the gather for the same reason
+  const bool head_lane = uh == 0 && (wave & 1) == 0;
+  float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto head_load = [&](int tile) __attribute__((always_inline)) {
+    const int s0 = tile * GT;
+    if (head_lane && s < min(GT, A.batch - s0)) {
+      const int sidx = A.idx[s0 + s];
+      if (nid == 0) {
+        hin[0] = A.actions[2 * (size_t)sidx];
+        hin[1] = A.actions[2 * (size_t)sidx + 1];
+        hin[2] = A.old_logp[sidx];
+        hin[3] = A.adv[sidx];
+      } else {
+        hin[0] = A.ret[sidx];
+      }
+    }
+  };
+  if (blockIdx.x < ntiles) {
+    gather_load(blockIdx.x);
+    head_load(blockIdx.x);
+  }
   stage_grad_weights(A.params, w);
 
   // MFMA tiles: lane (li, lk) = (lane & 15, lane >> 4). Wave w owns unit tiles ut = 2w, 2w + 1
@@ -650,7 +671,10 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
     __syncthreads();  // previous tile's LDS reads are done (and the weights are staged)
-    if (tile != blockIdx.x) gather_load(tile);
+    if (tile != blockIdx.x) {
+      gather_load(tile);
+      head_load(tile);
+    }
     {
       const int r = tid >> 3, q = tid & 7;
 #pragma unroll
@@ -659,7 +683,6 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
     __syncthreads();
     PSTAMP(1);
     const bool valid = s < nvalid;
-    const int sidx = valid ? A.idx[s0 + s] : 0;
     // GEMM-shaped layers: thread (ub, sb) owns 4 units (of the 128 actor|critic units) x 4 samples
     const int ub = tid >> 3, sb = tid & 7, gnet = ub >> 4, gu = 4 * (ub & 15), gs = 4 * sb;
     float* gt = tl + G_NET + gnet * G_NETSZ;  // this thread's net tile
@@ -735,8 +758,8 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
           for (int j = 0; j < H; j++) m = fmaf(w[W_AW + d * H + j], h[j], m);
           mu[d] = m + w[W_AB + d];
         }
-        a[0] = A.actions[2 * (size_t)sidx];
-        a[1] = A.actions[2 * (size_t)sidx + 1];
+        a[0] = hin[0];
+        a[1] = hin[1];
         float logp = 0.0f;
 #pragma unroll
         for (int d = 0; d < NA; d++) {
@@ -744,9 +767,9 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
           const float dv = a[d] - mu[d];
           logp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
         }
-        const float lr = logp - A.old_logp[sidx];
+        const float lr = logp - hin[2];
         const float r = expf(lr);
-        const float adv = (A.adv[sidx] - A.stats[0]) * A.stats[1];
+        const float adv = (hin[3] - A.stats[0]) * A.stats[1];
         const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
         const float l1 = adv * r, l2 = adv * rc;
         // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
@@ -770,7 +793,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
 #pragma unroll
         for (int j = 0; j < H; j++) v = fmaf(w[W_CW + j], h[j], v);
         v += w[W_CB];
-        const float R = A.ret[sidx];
+        const float R = hin[0];
         tl[G_GV + s] = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
         if (valid) la += (R - v) * (R - v);
       }
