@@ -80,6 +80,14 @@ __device__ __forceinline__ float ftanh(float x) {
   const float big = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
   return ax < 0.625f ? small : big;
 }
+// exp through the hardware exp2 (1 ulp, plus the rounding of x log2 e) and one dimension of the
+// DiagGaussian log-density with std exp(ls): -(a - mu)^2 / (2 exp(2 ls)) - ls - log sqrt(2 pi)
+// (log(exp(ls)) = ls, no division)
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504089f); }
+__device__ __forceinline__ float gauss_term(float a, float mu, float ls) {
+  const float dv = a - mu;
+  return -0.5f * dv * dv * fexp(-2.0f * ls) - ls - LOG_SQRT_2PI;
+}
 // out[j] = tanh(b[j] + W[j,:] . x) for the 64 units, written to an LDS column (stride cs).
 // W/b addresses are wave-uniform: scalar loads, x stays in VGPRs.
 template <int IN>
@@ -131,9 +139,7 @@ __device__ __forceinline__ float gauss_logp(const float a[NA], const float mu[NA
   float lp = 0.0f;
 #pragma unroll
   for (int d = 0; d < NA; d++) {
-    const float sigma = expf(p[ACKPPO_OFF_LOG_STD + d]);
-    const float dv = a[d] - mu[d];
-    lp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
+    lp += gauss_term(a[d], mu[d], p[ACKPPO_OFF_LOG_STD + d]);
   }
   return lp;
 }
@@ -762,13 +768,9 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
         a[1] = hin[1];
         float logp = 0.0f;
 #pragma unroll
-        for (int d = 0; d < NA; d++) {
-          const float sigma = expf(w[W_LS + d]);
-          const float dv = a[d] - mu[d];
-          logp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
-        }
+        for (int d = 0; d < NA; d++) logp += gauss_term(a[d], mu[d], w[W_LS + d]);
         const float lr = logp - hin[2];
-        const float r = expf(lr);
+        const float r = fexp(lr);
         const float adv = (hin[3] - A.stats[0]) * A.stats[1];
         const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
         const float l1 = adv * r, l2 = adv * rc;
@@ -777,10 +779,10 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
         const float glogp = valid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
 #pragma unroll
         for (int d = 0; d < NA; d++) {
-          const float sigma = expf(w[W_LS + d]);
+          const float inv_var = fexp(-2.0f * w[W_LS + d]);
           const float dv = a[d] - mu[d];
-          tl[G_GMU + d * GLDP + s] = glogp * dv / (sigma * sigma);
-          tl[G_GLOG + d * GLDP + s] = glogp * (dv * dv / (sigma * sigma) - 1.0f);
+          tl[G_GMU + d * GLDP + s] = glogp * dv * inv_var;
+          tl[G_GLOG + d * GLDP + s] = glogp * (dv * dv * inv_var - 1.0f);
         }
         if (valid) {
           la += -fminf(l1, l2);
@@ -1048,7 +1050,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
     const float r = sqrtf(-2.0f * logf(u1));
     const float z[NA] = {r * cosf(TWO_PI * u2), r * sinf(TWO_PI * u2)};
 #pragma unroll
-    for (int d = 0; d < NA; d++) a[d] = mu[d] + expf(w[W_LS + d]) * z[d];
+    for (int d = 0; d < NA; d++) a[d] = mu[d] + fexp(w[W_LS + d]) * z[d];
   }
   if (A.action) {
     A.action[2 * (size_t)e] = a[0];
@@ -1060,9 +1062,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
     float lp = 0.0f;
 #pragma unroll
     for (int d = 0; d < NA; d++) {  // gauss_logp with the staged log_std
-      const float sigma = expf(w[W_LS + d]);
-      const float dv = a[d] - mu[d];
-      lp += -(dv * dv) / (2.0f * sigma * sigma) - logf(sigma) - LOG_SQRT_2PI;
+      lp += gauss_term(a[d], mu[d], w[W_LS + d]);
     }
     A.log_prob[e] = lp;
   }
