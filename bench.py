@@ -50,16 +50,25 @@ def algorithmic_bytes_per_env_step() -> int:
 SETTLE_STEPS = 200
 
 
-def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat", graph=False):
+def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat", graph=False,
+            per_step=False):
+    """Times `steps` random-ctrl steps of the env shard. Default: ONE ackphys_rollout launch runs the
+    K pre-drawn action rows (every step computed and its outputs written, exactly K ackphys_step
+    calls' results -- tests/test_gpu_rollout.py); per_step=True: K ackphys_step launches (the call
+    pattern of a policy-in-the-loop RL step), graph=True: those K launches replayed from a hipGraph."""
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
                               env_offset=shard.env_offset(rank, n_env), variant=variant, scene=scene)
     sim.reset()
     pre = max(warmup, SETTLE_STEPS) if contacts else warmup
     actions = sim.random_actions(pre + steps, seed=seed)
     warmup = pre
-    for k in range(warmup):
-        sim.step(actions[k], want_info=False)
-    step_actions = actions[warmup:].unbind(0)  # per-step views, made before the timed region
+    if per_step or graph:
+        for k in range(warmup):
+            sim.step(actions[k], want_info=False)
+    elif warmup:
+        sim.rollout(actions[:warmup], want_info=False, per_step_outputs=False)
+    timed_actions = actions[warmup:]  # [K, N, 2], contiguous, resident before the timed region
+    step_actions = timed_actions.unbind(0)  # per-step views, made before the timed region
     g = None
     if graph:  # the K timed steps as one captured hipGraph (same launches, same buffers)
         snap = sim.state.clone(), sim.episode.clone()
@@ -78,9 +87,11 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     ev0.record(stream)
     if g is not None:
         g.replay()
-    else:
+    elif per_step:
         for k in range(steps):
             sim.step(step_actions[k], want_info=False)
+    else:
+        sim.rollout(timed_actions, want_info=False, per_step_outputs=False)
     ev1.record(stream)
     gathered = shard.gather_episode_stats(sim.episode, world)  # the per-rollout RCCL exchange
     torch.cuda.synchronize(device)
@@ -267,32 +278,46 @@ def main():
     ap.add_argument("--variant", default="auto", choices=["auto", "quad", "lane", "lane16"], help="step-kernel lane mapping")
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO-rollout leg (BASELINE configs[3])")
     ap.add_argument("--no-obstacles", action="store_true", help="skip the obstacle-scene leg (configs[4] world)")
-    ap.add_argument("--graph", action="store_true", help="replay the timed steps as one captured hipGraph")
+    ap.add_argument("--graph", action="store_true", help="replay the timed steps' launches as one captured hipGraph")
+    ap.add_argument("--per-step", action="store_true",
+                    help="time K ackphys_step launches instead of one ackphys_rollout launch of K steps")
     a = ap.parse_args()
     rank, world, local = shard.init()
     device = shard.device_for(local)
     torch.cuda.set_device(device)
     contacts = bool(a.contacts)
+    fused = not (a.per_step or a.graph)
     sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
-                                             variant=a.variant, graph=a.graph)
+                                             variant=a.variant, graph=a.graph, per_step=a.per_step)
     total_envs = a.envs * world
     value = total_envs * a.steps / elapsed
+
+    def per_step_leg(c, scene="flat"):
+        """the same workload as K ackphys_step launches (policy-in-the-loop call pattern)"""
+        _, el, km, _, _ = run_gpu(a.envs, a.steps, a.warmup, c, rank, world, device, variant=a.variant, scene=scene,
+                                  per_step=True)
+        return {"value": total_envs * a.steps / el, "ms_per_step": el * 1e3 / a.steps, "kernel_ms": km,
+                "note": "K ackphys_step launches (one per step) instead of one ackphys_rollout launch"}
+    per_step_launch = per_step_leg(contacts) if fused else None
     secondary = None
     if not a.no_secondary:
-        _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant)
+        _, el2, km2, _, _ = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant,
+                                    graph=a.graph, per_step=a.per_step)
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
-                     "kernel_ms": km2,
+                     "kernel_ms": km2, "per_step_launch": per_step_leg(not contacts) if fused else None,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup,
                      "flops": oracle_flops("configs[1] contacts off" if contacts else "configs[2] contacts on",
                                            total_envs * a.steps / el2)}
     ppo = None if a.no_ppo else run_ppo(a.envs, rank, world, device)
     obstacles = None
     if not a.no_obstacles:
-        _, el3, km3, rets3, _ = run_gpu(a.envs, a.steps, a.warmup, True, rank, world, device, scene="obstacles")
+        _, el3, km3, rets3, _ = run_gpu(a.envs, a.steps, a.warmup, True, rank, world, device, scene="obstacles",
+                                        graph=a.graph, per_step=a.per_step)
         obstacles = {"workload": f"v2 robot in ackermann_maze_flat.xml (38 static boxes), {a.envs} envs/GPU, "
                                  "random ctrl, contacts enabled, spawn at the scene's free cell",
                      "value": total_envs * a.steps / el3, "unit": "env-steps/s", "ms_per_step": el3 * 1e3 / a.steps,
-                     "kernel": "ackphys_step_obst_kernel", "kernel_ms": km3, "episodes": rets3,
+                     "kernel": "ackphys_rollout_obst_kernel" if fused else "ackphys_step_obst_kernel", "kernel_ms": km3,
+                     "per_step_launch": per_step_leg(True, "obstacles") if fused else None, "episodes": rets3,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS),
                      "flops": oracle_flops("configs[4] obstacle scene, contacts on", total_envs * a.steps / el3),
                      "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
@@ -301,20 +326,21 @@ def main():
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
     bpe = algorithmic_bytes_per_env_step()
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
-    kern = "ackphys_step_quad_kernel" if (a.variant == "quad" or (a.variant == "auto" and contacts)) \
-        else ("ackphys_step_kernel" if contacts else "ackphys_step_nc_kernel")
+    kern = "quad" if (a.variant == "quad" or (a.variant == "auto" and contacts)) else ("" if contacts else "nc")
+    kern = ("ackphys_rollout" if fused else "ackphys_step") + (f"_{kern}" if kern else "") + "_kernel"
     pmc = load_pmc(kern, contacts)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic = pmc.get("hbm_bytes_per_step") if pmc else None
     valu = None
-    if pmc and pmc.get("valu_insts_per_wave"):
+    if pmc and pmc.get("valu_insts_per_wave_step"):
         # one wave alone issues a dependent VALU op every ~4 cycles (MI355X_MICROARCH.md constants
         # table; tools/probes/launch_floor.py measures 4.1 cycles per op of a dependent FMA chain)
-        valu = {"insts_per_wave": pmc["valu_insts_per_wave"], "waves": pmc["SQ_WAVES"],
-                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave"] * 4 / (kern_ms * 1e-3 * 2.4e9),
+        valu = {"insts_per_wave_step": pmc["valu_insts_per_wave_step"], "waves": pmc["SQ_WAVES"],
+                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave_step"] * 4 / (kern_ms * 1e-3 * 2.4e9),
                 "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave "
                         "dependent-op rate (4 cyc/op, 2.4 GHz), per-wave average over the kernel's waves "
                         "(contacts off: dynamics, observation and prep waves); the rest is dependency/memory "
-                        "latency and the ~2.3 us launch floor of an empty kernel of this grid"}
+                        "latency (and, per ackphys_step launch, the ~2.3 us launch floor of an empty kernel of "
+                        "this grid)"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -331,9 +357,19 @@ def main():
                          "flops": oracle_flops("configs[2] contacts on" if contacts else "configs[1] contacts off",
                                                value),
                          "algorithmic_bytes_per_env_step": bpe,
+                         "unit_of_work": (f"one step of {a.envs} envs: achieved = {bpe} B x envs / kernel_ms, "
+                                          "traffic = PMC HBM bytes per step (the profiled launch's bytes / its "
+                                          "steps); " + (f"one launch runs all {a.steps} timed steps, so per launch "
+                                                        "both scale by the step count" if fused else
+                                                        "one launch per step")),
                          "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation + 64 prep "
                                  "waves (lane mapping, contacts off), i.e. 192 of 1024 SIMDs; HBM fraction is "
                                  "tiny by construction"},
+            "timing": ("one ackphys_rollout launch of the K timed steps (pre-drawn actions resident in HBM; every "
+                       "step computed and its outputs written)" if fused else
+                       ("K ackphys_step launches replayed from a hipGraph" if a.graph else
+                        "K ackphys_step launches")),
+            "per_step_launch": per_step_launch,
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
             "obstacles": obstacles,
         }

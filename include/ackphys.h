@@ -97,6 +97,17 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
                  uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags, uint64_t seed,
                  void* stream);
 
+/* k_steps consecutive steps of all N envs in ONE launch, for open-loop action sequences (the
+ * random-ctrl benchmark configs, replayed action streams, scripted controllers): exactly
+ * k_steps ackphys_step calls with actions[k] ([K][N][2]), same kernels' arithmetic, same
+ * auto-reset and episode statistics. per_step_outputs = 0: obs/reward/term/trunc/terminal_obs/info
+ * are the single-step shapes, overwritten by every step (left holding step K-1's); != 0: they are
+ * [K][...] and step k writes slice k (a rollout buffer). With ACKPHYS_POSTSTEP_OBS the steps are
+ * K single-step launches. Replaces a Python loop of env.step over a precomputed action array. */
+int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* state, float* obs, float* reward,
+                    uint8_t* term, uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags,
+                    uint64_t seed, int per_step_outputs, void* stream);
+
 /* Reset the envs whose mask byte is non-zero (mask NULL = all) (replaces
  * AckermannRobotEnv.reset): spawner pose, zero velocities, Philox(seed, env, episode) goal,
  * observation at the reset state. */

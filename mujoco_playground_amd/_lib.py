@@ -85,7 +85,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     return _hipcc(LIB_PATH, SOURCES, verbose, force, tuple(PHYS_FLAGS))
 
 
-EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_reset",
+EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_rollout",
+           "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
 PPO_EXPORTS = ["ackppo_act", "ackppo_act_boot", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
@@ -116,6 +117,7 @@ def lib():
     L.ackphys_set_variant.argtypes = [P, i32]
     L.ackphys_set_env_params.argtypes = [P, C.POINTER(EnvParams)]
     L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, P, u32, u64, P]
+    L.ackphys_rollout.argtypes = [P, i32, P, P, P, P, P, P, P, P, P, u32, u64, i32, P]
     L.ackphys_reset.argtypes = [P, P, u64, P, P, P]
     L.ackphys_random_actions.argtypes = [P, P, i32, u64, u32, P]
     L.ackphys_model_fnv.restype = u64

@@ -121,7 +121,25 @@ struct Args {
   uint64_t seed;
   int64_t env_offset;
   int epw;  // lane kernel: envs per 64-lane wave (lanes >= epw idle)
+  int ksteps = 1;    // rollout kernels: consecutive steps per launch (action k at action + 2kN)
+  int per_step = 0;  // rollout kernels: step k's outputs in slice k of obs/reward/term/trunc/tobs/info
 };
+
+// Args of step k of a rollout launch: the k-th action row and, with per_step, the k-th output slices
+__device__ __forceinline__ Args step_args(const Args& A, int k) {
+  Args B = A;
+  const size_t n = (size_t)A.n, kk = (size_t)k;
+  B.action = A.action + kk * 2 * n;
+  if (A.per_step) {
+    B.obs = A.obs + kk * NOBS * n;
+    B.reward = A.reward + kk * n;
+    B.term = A.term + kk * n;
+    B.trunc = A.trunc + kk * n;
+    if (A.tobs) B.tobs = A.tobs + kk * NOBS * n;
+    if (A.info) B.info = A.info + kk * 4 * n;
+  }
+  return B;
+}
 
 // ------------------------------------------------------------------ SoA buffer access
 // Every per-env array is [rows][n] (or [n] / [n][2]). Accesses go through a buffer descriptor
@@ -2416,6 +2434,28 @@ extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_ke
   step_split<1, AK_NC_PW>(A);
 }
 
+// Rollout kernels (ackphys_rollout): A.ksteps consecutive steps of the same envs in one launch,
+// each one exactly the single-step kernel's work with its own action row and output slices. The
+// state goes through HBM (L1/L2 hits) between steps as between launches; what a step costs less is
+// the launch: dispatch, wave start-up and the drain of the whole grid. Step k + 1's prep and
+// observation waves load the state the dynamics wave stored in step k: with the prep wave that
+// store precedes barrier 0 of step k + 1, which the loading waves pass first (same CU, so the
+// workgroup-scope fence of the barrier suffices); without it an explicit barrier separates them.
+extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_rollout_nc_kernel(Args A) {
+#pragma unroll 1
+  for (int k = 0; k < A.ksteps; k++) {
+    if (!AK_XCH && k) __syncthreads();
+    step_split<1, AK_NC_PW>(step_args(A, k));
+  }
+}
+extern "C" __global__ void __launch_bounds__(64 * (2 + (AK_XCH ? 1 : 0)), 1) ackphys_rollout_kernel(Args A) {
+#pragma unroll 1
+  for (int k = 0; k < A.ksteps; k++) {
+    if (!AK_XCH && k) __syncthreads();
+    step_split<0, 1>(step_args(A, k));
+  }
+}
+
 template <int SC>
 __device__ __forceinline__ void reset_body(const uint8_t* mask, float* state, float* obs, int n, uint64_t seed,
                                            int64_t env_offset, const EnvParams& prm) {
@@ -2571,6 +2611,10 @@ int ackphys_set_env_offset(ackphys_t* ctx, int64_t off) {
   return ACKPHYS_OK;
 }
 
+// One launch of a.ksteps steps: the rollout kernels when ksteps > 1 (the post-step-observation mode
+// has none: its K single-step launches run back to back on the stream, same results).
+static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream);
+
 int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, float* reward, uint8_t* term,
                  uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags, uint64_t seed,
                  void* stream) {
@@ -2578,9 +2622,49 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     return fail(ACKPHYS_EINVAL, "ackphys_step: NULL argument");
   DeviceGuard dg(ctx->device);
   if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
-  hipError_t e;
   ak::Args a{action, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
              ctx->env_offset, 64};
+  return launch_steps(ctx, a, flags, stream);
+}
+
+int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* state, float* obs, float* reward,
+                    uint8_t* term, uint8_t* trunc, float* terminal_obs, float* info, float* episode, uint32_t flags,
+                    uint64_t seed, int per_step_outputs, void* stream) {
+  if (!ctx || !actions || !state || !obs || !reward || !term || !trunc)
+    return fail(ACKPHYS_EINVAL, "ackphys_rollout: NULL argument");
+  if (k_steps <= 0) return fail(ACKPHYS_EINVAL, "ackphys_rollout: k_steps must be positive");
+  DeviceGuard dg(ctx->device);
+  if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
+  ak::Args a{actions, state, obs, reward, term, trunc, terminal_obs, info, episode, ctx->prm, ctx->n_env, flags, seed,
+             ctx->env_offset, 64};
+  a.ksteps = k_steps;
+  a.per_step = per_step_outputs ? 1 : 0;
+  if (flags & ACKPHYS_POSTSTEP_OBS) {
+    const size_t n = (size_t)ctx->n_env;
+    for (int k = 0; k < k_steps; k++) {
+      ak::Args b = a;
+      b.ksteps = 1;
+      b.per_step = 0;
+      b.action = actions + (size_t)k * 2 * n;
+      if (a.per_step) {
+        b.obs = obs + (size_t)k * ACKPHYS_NOBS * n;
+        b.reward = reward + (size_t)k * n;
+        b.term = term + (size_t)k * n;
+        b.trunc = trunc + (size_t)k * n;
+        if (terminal_obs) b.tobs = terminal_obs + (size_t)k * ACKPHYS_NOBS * n;
+        if (info) b.info = info + (size_t)k * 4 * n;
+      }
+      const int rc = launch_steps(ctx, b, flags, stream);
+      if (rc) return rc;
+    }
+    return ACKPHYS_OK;
+  }
+  return launch_steps(ctx, a, flags, stream);
+}
+
+static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream) {
+  hipError_t e;
+  const bool multi = a.ksteps > 1;
   // AUTO: with contacts the quad mapping wins (contact rows dominate and split 4 ways); without
   // contacts the replicated serial core dominates and one lane per env is marginally faster.
   const bool quad = ctx->variant == ACKPHYS_VARIANT_QUAD ||
@@ -2592,13 +2676,15 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_obst_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(ackphys_step_obst_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(multi ? ackphys_rollout_obst_kernel : ackphys_step_obst_kernel, dim3(blocks), dim3(128), 0,
+                         (hipStream_t)stream, a);
   } else if (quad) {
     int blocks = (ctx->n_env + 15) / 16;
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_quad_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(ackphys_step_quad_kernel, dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(multi ? ackphys_rollout_quad_kernel : ackphys_step_quad_kernel, dim3(blocks), dim3(128), 0,
+                         (hipStream_t)stream, a);
   } else {
     a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
     const int pw = (flags & (ACKPHYS_POSTSTEP_OBS | ACKPHYS_CONTACTS)) ? 1 : AK_NC_PW;
@@ -2606,10 +2692,11 @@ int ackphys_step(ackphys_t* ctx, const float* action, float* state, float* obs, 
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else if (flags & ACKPHYS_CONTACTS)
-      hipLaunchKernelGGL(ackphys_step_kernel, dim3(blocks), dim3(64 * (2 + (AK_XCH ? 1 : 0))), 0, (hipStream_t)stream,
-                         a);
+      hipLaunchKernelGGL(multi ? ackphys_rollout_kernel : ackphys_step_kernel, dim3(blocks),
+                         dim3(64 * (2 + (AK_XCH ? 1 : 0))), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(ackphys_step_nc_kernel, dim3(blocks), dim3(LANE_THREADS), 0, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(multi ? ackphys_rollout_nc_kernel : ackphys_step_nc_kernel, dim3(blocks), dim3(LANE_THREADS),
+                         0, (hipStream_t)stream, a);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_step_kernel launch");

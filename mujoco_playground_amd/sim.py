@@ -117,6 +117,43 @@ class BatchedAckermannSim:
             _lib.check(rc, "ackphys_step")
         return self.obs_soa, self.reward, self.term, self.trunc
 
+    def rollout(self, actions: torch.Tensor, autoreset: bool = True, want_info: bool = True,
+                want_terminal: bool = True, track_episodes: bool = True, per_step_outputs: bool = True):
+        """K steps of an open-loop action sequence in one launch (ackphys_rollout): the same as
+        K calls of `step(actions[k])`. actions [K,N,2] float32 on device. With per_step_outputs the
+        result is freshly allocated [K,...] tensors (obs [K,79,N], reward [K,N], term, trunc; info
+        [K,4,N] and terminal obs [K,79,N] when asked for); without, the sim's single-step buffers
+        (holding step K-1's outputs) are returned, as after K `step` calls."""
+        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if actions.dim() != 3 or actions.shape[1:] != (self.n, 2) or actions.shape[0] < 1:
+            raise ValueError(f"actions must be [K, {self.n}, 2], got {tuple(actions.shape)}")
+        k = int(actions.shape[0])
+        flags = self.flags | (AUTORESET if autoreset else 0)
+        term_on = autoreset and want_terminal
+        if per_step_outputs:
+            f32, u8, d = torch.float32, torch.uint8, self.device
+            obs = torch.empty(k, NOBS, self.n, dtype=f32, device=d)
+            rew = torch.empty(k, self.n, dtype=f32, device=d)
+            term = torch.empty(k, self.n, dtype=u8, device=d)
+            trunc = torch.empty(k, self.n, dtype=u8, device=d)
+            # terminal obs rows are written only for done envs: zero-filled like the sim's buffer
+            tobs = torch.zeros(k, NOBS, self.n, dtype=f32, device=d) if term_on else None
+            info = torch.empty(k, 4, self.n, dtype=f32, device=d) if want_info else None
+        else:
+            obs, rew, term, trunc = self.obs_soa, self.reward, self.term, self.trunc
+            tobs = self.terminal_obs_soa if term_on else None
+            info = self.info if want_info else None
+        rc = _lib.lib().ackphys_rollout(
+            self._ctx, k, actions.data_ptr(), self._c["state"], _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+            _ptr(tobs), _ptr(info), self._c["episode"] if track_episodes else None, flags, self.seed, int(per_step_outputs),
+            _raw_stream(self._dev_index))
+        if rc:
+            _lib.check(rc, "ackphys_rollout")
+        if per_step_outputs:
+            self.last_rollout = {"terminal_obs": tobs, "info": info}
+        return obs, rew, term, trunc
+
     def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:
         """[K, N, 2] i.i.d. U[-1,1) actions from Philox(seed; env, step) on device."""
         out = torch.empty(k_steps, self.n, 2, dtype=torch.float32, device=self.device)

@@ -1,12 +1,13 @@
 """rocprofv3 PMC passes for the step kernels -> gpurun_out/pmc_latest.json (run on the GPU box).
 
-For each workload (contacts off -> ackphys_step_nc_kernel, contacts on -> ackphys_step_quad_kernel,
-the kernels bench.py's AUTO mapping runs) three separate passes, kernel-trace only, no
-sys/runtime trace:
+For each workload (contacts off -> ackphys_rollout_nc_kernel, contacts on -> ackphys_rollout_quad_kernel,
+the kernels bench.py's AUTO mapping runs; one launch = the K timed steps) three separate passes,
+kernel-trace only, no sys/runtime trace:
   FETCH_SIZE, WRITE_SIZE (HBM bytes; they do not fit one TCC pass on gfx950),
   SQ_INSTS_VALU + SQ_INSTS_SALU + SQ_WAVES (instruction mix, one SQ pass).
 Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B requests at 64 B for
-lane-contiguous streaming reads -> doubled; WRITE_SIZE taken as reported.
+lane-contiguous streaming reads -> doubled; WRITE_SIZE taken as reported. The counters of the
+timed launch (the kernel's last dispatch) are divided by its K steps: bytes and instructions per step.
     python3 tools/profile_pmc.py
 """
 import csv
@@ -17,22 +18,25 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {0: "ackphys_step_nc_kernel", 1: "ackphys_step_quad_kernel"}
+KERNELS = {0: "ackphys_rollout_nc_kernel", 1: "ackphys_rollout_quad_kernel"}
+K = 60  # timed steps = steps of the profiled launch
 
 
 def run_pass(counters, out, contacts):
     os.makedirs(out, exist_ok=True)
     cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
            "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
-           "--steps", "60", "--warmup", "5", "--contacts", str(contacts)]
+           "--no-obstacles", "--steps", str(K), "--warmup", "5", "--contacts", str(contacts)]
     env = dict(os.environ, TMPDIR="/tmp")
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, stdout=subprocess.DEVNULL)
-    vals = {c: [] for c in counters}
+    vals = {c: {} for c in counters}  # counter -> dispatch id -> value (summed over the rows of a dispatch)
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if row.get("Kernel_Name", "").startswith(KERNELS[contacts]) and row.get("Counter_Name") in vals:
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {c: (sorted(v)[len(v) // 2] if v else None) for c, v in vals.items()}  # median dispatch
+                d = int(row.get("Dispatch_Id", 0))
+                v = vals[row["Counter_Name"]]
+                v[d] = v.get(d, 0.0) + float(row["Counter_Value"])
+    return {c: (v[max(v)] if v else None) for c, v in vals.items()}  # the timed launch = the last dispatch
 
 
 def main():
@@ -43,12 +47,13 @@ def main():
         w = run_pass(["WRITE_SIZE"], out + "_write", contacts)["WRITE_SIZE"]
         sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts)
         res[kern] = {
-            "contacts": bool(contacts), "FETCH_SIZE_kB_median": f, "WRITE_SIZE_kB_median": w,
+            "contacts": bool(contacts), "launch_steps": K, "FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w,
             "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if (f is not None and w is not None) else None,
+            "hbm_bytes_per_step": (2 * f * 1024 + w * 1024) / K if (f is not None and w is not None) else None,
             "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
-            "algorithmic_bytes_per_launch": 690 * 4096,
+            "algorithmic_bytes_per_step": 690 * 4096,
             "SQ_INSTS_VALU": sq["SQ_INSTS_VALU"], "SQ_INSTS_SALU": sq["SQ_INSTS_SALU"], "SQ_WAVES": sq["SQ_WAVES"],
-            "valu_insts_per_wave": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]) if sq["SQ_WAVES"] else None,
+            "valu_insts_per_wave_step": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] / K) if sq["SQ_WAVES"] else None,
         }
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
