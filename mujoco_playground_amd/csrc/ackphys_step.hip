@@ -123,6 +123,11 @@ struct Args {
   int epw;  // lane kernel: envs per 64-lane wave (lanes >= epw idle)
   int ksteps = 1;    // rollout kernels: consecutive steps per launch (action k at action + 2kN)
   int per_step = 0;  // rollout kernels: step k's outputs in slice k of obs/reward/term/trunc/tobs/info
+  // lane rollout kernels: LDS mirror of the state words ([NSTATE][64 PW]) between the steps of a
+  // launch: sm_in = this step reads its state there (not HBM), sm_out = the dynamics wave leaves
+  // the post-step state there instead of storing it (every step but the launch's last)
+  float* sm = nullptr;
+  int sm_in = 0, sm_out = 0;
 };
 
 // Args of step k of a rollout launch: the k-th action row and, with per_step, the k-th output slices
@@ -207,11 +212,18 @@ __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }
 #define AK_POLYTRIG 1
 #endif
 #if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt
-__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
-__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
-__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-#define AK_PIVOT_RSQ(x) __builtin_amdgcn_rsqf(x)
+// An argument that is a compile-time constant once inlined (model constants: the constant blocks
+// of the mass matrix and of its factors, impedance and regulariser terms) takes the correctly
+// rounded form, which the compiler folds; the hardware builtins are opaque to constant folding and
+// otherwise run (or, in a rollout kernel's step loop, are hoisted and held in registers) per step.
+#define AK_HW_OR_FOLD(x, folded, hw) (__builtin_constant_p(x) ? (folded) : (hw))
+__device__ __forceinline__ float frcp(float x) { return AK_HW_OR_FOLD(x, 1.0f / x, __builtin_amdgcn_rcpf(x)); }
+__device__ __forceinline__ float fdiv(float a, float b) {
+  return AK_HW_OR_FOLD(b, a * (1.0f / b), a * __builtin_amdgcn_rcpf(b));
+}
+__device__ __forceinline__ float frsq(float x) { return AK_HW_OR_FOLD(x, 1.0f / sqrtf(x), __builtin_amdgcn_rsqf(x)); }
+__device__ __forceinline__ float fsqrt(float x) { return AK_HW_OR_FOLD(x, sqrtf(x), __builtin_amdgcn_sqrtf(x)); }
+#define AK_PIVOT_RSQ(x) frsq(x)
 #else
 __device__ __forceinline__ float frcp(float x) { return 1.0f / x; }
 __device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
@@ -1931,7 +1943,8 @@ __device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_
 // reset env e: writes state words + observation
 template <int SC>
 __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint32_t vo, uint64_t seed, int64_t genv,
-                                          uint32_t episode, const EnvParams& prm) {
+                                          uint32_t episode, const EnvParams& prm, float* smw = nullptr,
+                                          int sms = 0) {
   float qpos[13], qvel[NV], warm[NV];
   reset_pose<SC>(qpos, qvel, warm);
   float gx, gy;
@@ -1954,6 +1967,18 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
   for (int k = 0; k < 3; k++) stf(state, ST_REF + k, vo, ref[k]);
   stf(state, ST_STEP, vo, __uint_as_float(0u));
   stf(state, ST_EPIS, vo, __uint_as_float(episode));
+  if (smw) {  // rollout: the same words into the LDS state mirror for the launch's next step
+#pragma unroll
+    for (int i = 0; i < 13; i++) smw[(ST_QPOS + i) * sms] = qpos[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) { smw[(ST_QVEL + i) * sms] = 0.0f; smw[(ST_WARM + i) * sms] = 0.0f; }
+    smw[ST_GOAL * sms] = gx;
+    smw[(ST_GOAL + 1) * sms] = gy;
+#pragma unroll
+    for (int k = 0; k < 3; k++) smw[(ST_REF + k) * sms] = ref[k];
+    smw[ST_STEP * sms] = __uint_as_float(0u);
+    smw[ST_EPIS * sms] = __uint_as_float(episode);
+  }
   observe<SC>(qpos, q, R, gx, gy, ref, obs, vo, prm);
 }
 
@@ -2133,16 +2158,34 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
     if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; }
     __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
+  const int sms = 64 * npair;  // word stride of the LDS state mirror
+  float* const smw = A.sm ? A.sm + slot : nullptr;
   if (valid) {
     STAMP(0);
+    if (A.sm_in) {
 #pragma unroll
-    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+      for (int i = 0; i < 13; i++) qpos[i] = smw[(ST_QPOS + i) * sms];
 #pragma unroll
-    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+      for (int i = 0; i < NV; i++) qvel[i] = smw[(ST_QVEL + i) * sms];
 #pragma unroll
-    for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
-    step = __float_as_uint(ldf(st, ST_STEP, vo));
-    episode = __float_as_uint(ldf(st, ST_EPIS, vo));
+      for (int i = 0; i < NV; i++) warm[i] = smw[(ST_WARM + i) * sms];
+      step = __float_as_uint(smw[ST_STEP * sms]);
+      episode = __float_as_uint(smw[ST_EPIS * sms]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+      for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+#pragma unroll
+      for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
+      step = __float_as_uint(ldf(st, ST_STEP, vo));
+      episode = __float_as_uint(ldf(st, ST_EPIS, vo));
+      if (A.sm_out) {  // first step of a rollout launch: the words only a reset changes, into the mirror
+#pragma unroll
+        for (int k = 0; k < 5; k++) smw[(ST_GOAL + k) * sms] = ldf(st, ST_GOAL + k, vo);
+        smw[ST_EPIS * sms] = __uint_as_float(episode);
+      }
+    }
     if constexpr (!AK_XCH) {
       const Soa act = soa(A.action, 2, n);
       const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
@@ -2195,7 +2238,18 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   if (!valid) return;
   STAMP(9);
   if (sh_reset[slot]) {
-    reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm);
+    reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm, A.sm_out ? smw : nullptr,
+                 sms);
+    return;
+  }
+  if (A.sm_out) {  // rollout, not the launch's last step: the state stays in LDS
+#pragma unroll
+    for (int i = 0; i < 13; i++) smw[(ST_QPOS + i) * sms] = qpos[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) smw[(ST_QVEL + i) * sms] = qvel[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) smw[(ST_WARM + i) * sms] = warm[i];
+    smw[ST_STEP * sms] = __uint_as_float(step + 1);
     return;
   }
 #pragma unroll
@@ -2223,16 +2277,20 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
   float ep0 = 0.0f, ep1 = 0.0f, ep2 = 0.0f, ep3 = 0.0f;
   const Soa ep = soa(A.ep, 4, n);
   if (valid) {
+    // rollout steps after a launch's first read the LDS state mirror instead (same words)
+    const float* smr = A.sm_in ? A.sm + slot : nullptr;
+    const int sms = 64 * npair;
+    auto ld = [&](int w) __attribute__((always_inline)) { return smr ? smr[w * sms] : ldf(st, w, vo); };
 #pragma unroll
-    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+    for (int i = 0; i < 13; i++) qpos[i] = ld(ST_QPOS + i);
     float qvel[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
-    gx = ldf(st, ST_GOAL, vo);
-    gy = ldf(st, ST_GOAL + 1, vo);
+    for (int i = 0; i < NV; i++) qvel[i] = ld(ST_QVEL + i);
+    gx = ld(ST_GOAL);
+    gy = ld(ST_GOAL + 1);
 #pragma unroll
-    for (int k = 0; k < 3; k++) ref[k] = ldf(st, ST_REF + k, vo);
-    step = __float_as_uint(ldf(st, ST_STEP, vo));
+    for (int k = 0; k < 3; k++) ref[k] = ld(ST_REF + k);
+    step = __float_as_uint(ld(ST_STEP));
     if (A.ep) { ep0 = ldf(ep, 0, vo); ep1 = ldf(ep, 1, vo); ep2 = ldf(ep, 2, vo); ep3 = ldf(ep, 3, vo); }
     // mj_checkPos / mj_checkVel on the loaded state (the same test as wave 0's)
 #pragma unroll
@@ -2337,10 +2395,12 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
   bool bad = false;
   if (valid) {
     float qvel[NV];
+    const float* smr = A.sm_in ? A.sm + lane : nullptr;  // rollout: LDS state mirror (one wave pair)
+    auto ld = [&](int w) __attribute__((always_inline)) { return smr ? smr[w * 64] : ldf(st, w, vo); };
 #pragma unroll
-    for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+    for (int i = 0; i < 13; i++) qpos[i] = ld(ST_QPOS + i);
 #pragma unroll
-    for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+    for (int i = 0; i < NV; i++) qvel[i] = ld(ST_QVEL + i);
     const Soa act = soa(A.action, 2, n);
     const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
     float ctrl[3];
@@ -2441,19 +2501,29 @@ extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_ke
 // observation waves load the state the dynamics wave stored in step k: with the prep wave that
 // store precedes barrier 0 of step k + 1, which the loading waves pass first (same CU, so the
 // workgroup-scope fence of the barrier suffices); without it an explicit barrier separates them.
-extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_rollout_nc_kernel(Args A) {
+#ifndef AK_ROLL_SM
+#define AK_ROLL_SM 1  // lane rollout kernels: state between steps in an LDS mirror, not HBM
+#endif
+template <int NC, int PW>
+__device__ __forceinline__ void rollout_split(const Args& A) {
+  __shared__ float sm[AK_ROLL_SM ? NSTATE * 64 * PW : 1];
 #pragma unroll 1
   for (int k = 0; k < A.ksteps; k++) {
     if (!AK_XCH && k) __syncthreads();
-    step_split<1, AK_NC_PW>(step_args(A, k));
+    Args B = step_args(A, k);
+    if constexpr (AK_ROLL_SM) {
+      B.sm = sm;
+      B.sm_in = k > 0;
+      B.sm_out = k + 1 < A.ksteps;
+    }
+    step_split<NC, PW>(B);
   }
 }
+extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_rollout_nc_kernel(Args A) {
+  rollout_split<1, AK_NC_PW>(A);
+}
 extern "C" __global__ void __launch_bounds__(64 * (2 + (AK_XCH ? 1 : 0)), 1) ackphys_rollout_kernel(Args A) {
-#pragma unroll 1
-  for (int k = 0; k < A.ksteps; k++) {
-    if (!AK_XCH && k) __syncthreads();
-    step_split<0, 1>(step_args(A, k));
-  }
+  rollout_split<0, 1>(A);
 }
 
 template <int SC>
