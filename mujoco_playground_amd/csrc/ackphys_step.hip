@@ -126,8 +126,14 @@ struct Args {
   // lane rollout kernels: LDS mirror of the state words ([NSTATE][64 PW]) between the steps of a
   // launch: sm_in = this step reads its state there (not HBM), sm_out = the dynamics wave leaves
   // the post-step state there instead of storing it (every step but the launch's last)
-  float* sm = nullptr;
+  float* sm = nullptr;       // the mirror this step reads (sm_in)
+  float* sm_next = nullptr;  // the mirror the next step reads, written by this step (sm_out); double
+                             // buffered, so the dynamics wave can write it before barrier 1
   int sm_in = 0, sm_out = 0;
+  // contacts-off rollout kernel: the prep wave computes step k + 1's controller output (a function of
+  // the action alone) during step k from next_action into nctrl (LDS [3][64]); read when sm_in
+  const float* next_action = nullptr;
+  float* nctrl = nullptr;
 };
 
 // Args of step k of a rollout launch: the k-th action row and, with per_step, the k-th output slices
@@ -2158,8 +2164,9 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
     if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; }
     __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
-  const int sms = 64 * npair;  // word stride of the LDS state mirror
+  const int sms = 64 * npair;  // word stride of the LDS state mirrors
   float* const smw = A.sm ? A.sm + slot : nullptr;
+  float* const smn = A.sm_next ? A.sm_next + slot : nullptr;
   if (valid) {
     STAMP(0);
     if (A.sm_in) {
@@ -2180,10 +2187,15 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
       for (int i = 0; i < NV; i++) warm[i] = ldf(st, ST_WARM + i, vo);
       step = __float_as_uint(ldf(st, ST_STEP, vo));
       episode = __float_as_uint(ldf(st, ST_EPIS, vo));
-      if (A.sm_out) {  // first step of a rollout launch: the words only a reset changes, into the mirror
+      if (A.sm_out) {  // first step of a rollout launch: the words only a reset changes, into both mirrors
 #pragma unroll
-        for (int k = 0; k < 5; k++) smw[(ST_GOAL + k) * sms] = ldf(st, ST_GOAL + k, vo);
+        for (int k = 0; k < 5; k++) {
+          const float v = ldf(st, ST_GOAL + k, vo);
+          smw[(ST_GOAL + k) * sms] = v;
+          smn[(ST_GOAL + k) * sms] = v;
+        }
         smw[ST_EPIS * sms] = __uint_as_float(episode);
+        smn[ST_EPIS * sms] = __uint_as_float(episode);
       }
     }
     if constexpr (!AK_XCH) {
@@ -2228,6 +2240,15 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
       dynamics<NC>(S, qpos, u, wu, R, ctrl, A.flags, res);
     }
     euler_advance(u, res, R, qpos, qvel, warm);
+    if (A.sm_out) {  // rollout, not the launch's last step: the next step reads the state from LDS
+#pragma unroll
+      for (int i = 0; i < 13; i++) smn[(ST_QPOS + i) * sms] = qpos[i];
+#pragma unroll
+      for (int i = 0; i < NV; i++) smn[(ST_QVEL + i) * sms] = qvel[i];
+#pragma unroll
+      for (int i = 0; i < NV; i++) smn[(ST_WARM + i) * sms] = warm[i];
+      smn[ST_STEP * sms] = __uint_as_float(step + 1);
+    }
     STAMP(8);
   }
   sh_bad[slot] = redo ? 1 : 0;
@@ -2238,20 +2259,15 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   if (!valid) return;
   STAMP(9);
   if (sh_reset[slot]) {
-    reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm, A.sm_out ? smw : nullptr,
+    reset_env<0>(st, soa(A.obs, NOBS, n), vo, A.seed, A.env_offset + e, episode + 1, A.prm, A.sm_out ? smn : nullptr,
                  sms);
+    if (A.sm_out) {  // the reset words into the other mirror too (goal, odometry reference, episode live on)
+#pragma unroll
+      for (int w = 0; w < NSTATE; w++) smw[w * sms] = smn[w * sms];
+    }
     return;
   }
-  if (A.sm_out) {  // rollout, not the launch's last step: the state stays in LDS
-#pragma unroll
-    for (int i = 0; i < 13; i++) smw[(ST_QPOS + i) * sms] = qpos[i];
-#pragma unroll
-    for (int i = 0; i < NV; i++) smw[(ST_QVEL + i) * sms] = qvel[i];
-#pragma unroll
-    for (int i = 0; i < NV; i++) smw[(ST_WARM + i) * sms] = warm[i];
-    smw[ST_STEP * sms] = __uint_as_float(step + 1);
-    return;
-  }
+  if (A.sm_out) return;  // the state is in the next step's LDS mirror
 #pragma unroll
   for (int i = 0; i < 13; i++) stf(st, ST_QPOS + i, vo, qpos[i]);
 #pragma unroll
@@ -2278,19 +2294,30 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
   const Soa ep = soa(A.ep, 4, n);
   if (valid) {
     // rollout steps after a launch's first read the LDS state mirror instead (same words)
-    const float* smr = A.sm_in ? A.sm + slot : nullptr;
-    const int sms = 64 * npair;
-    auto ld = [&](int w) __attribute__((always_inline)) { return smr ? smr[w * sms] : ldf(st, w, vo); };
-#pragma unroll
-    for (int i = 0; i < 13; i++) qpos[i] = ld(ST_QPOS + i);
     float qvel[NV];
+    if (A.sm_in) {
+      const float* smr = A.sm + slot;
+      const int sms = 64 * npair;
 #pragma unroll
-    for (int i = 0; i < NV; i++) qvel[i] = ld(ST_QVEL + i);
-    gx = ld(ST_GOAL);
-    gy = ld(ST_GOAL + 1);
+      for (int i = 0; i < 13; i++) qpos[i] = smr[(ST_QPOS + i) * sms];
 #pragma unroll
-    for (int k = 0; k < 3; k++) ref[k] = ld(ST_REF + k);
-    step = __float_as_uint(ld(ST_STEP));
+      for (int i = 0; i < NV; i++) qvel[i] = smr[(ST_QVEL + i) * sms];
+      gx = smr[ST_GOAL * sms];
+      gy = smr[(ST_GOAL + 1) * sms];
+#pragma unroll
+      for (int k = 0; k < 3; k++) ref[k] = smr[(ST_REF + k) * sms];
+      step = __float_as_uint(smr[ST_STEP * sms]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+      for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+      gx = ldf(st, ST_GOAL, vo);
+      gy = ldf(st, ST_GOAL + 1, vo);
+#pragma unroll
+      for (int k = 0; k < 3; k++) ref[k] = ldf(st, ST_REF + k, vo);
+      step = __float_as_uint(ldf(st, ST_STEP, vo));
+    }
     if (A.ep) { ep0 = ldf(ep, 0, vo); ep1 = ldf(ep, 1, vo); ep2 = ldf(ep, 2, vo); ep3 = ldf(ep, 3, vo); }
     // mj_checkPos / mj_checkVel on the loaded state (the same test as wave 0's)
 #pragma unroll
@@ -2395,18 +2422,30 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
   bool bad = false;
   if (valid) {
     float qvel[NV];
-    const float* smr = A.sm_in ? A.sm + lane : nullptr;  // rollout: LDS state mirror (one wave pair)
-    auto ld = [&](int w) __attribute__((always_inline)) { return smr ? smr[w * 64] : ldf(st, w, vo); };
+    if (A.sm_in) {  // rollout: LDS state mirror (one wave pair)
+      const float* smr = A.sm + lane;
 #pragma unroll
-    for (int i = 0; i < 13; i++) qpos[i] = ld(ST_QPOS + i);
+      for (int i = 0; i < 13; i++) qpos[i] = smr[(ST_QPOS + i) * 64];
 #pragma unroll
-    for (int i = 0; i < NV; i++) qvel[i] = ld(ST_QVEL + i);
-    const Soa act = soa(A.action, 2, n);
-    const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+      for (int i = 0; i < NV; i++) qvel[i] = smr[(ST_QVEL + i) * 64];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 13; i++) qpos[i] = ldf(st, ST_QPOS + i, vo);
+#pragma unroll
+      for (int i = 0; i < NV; i++) qvel[i] = ldf(st, ST_QVEL + i, vo);
+    }
     float ctrl[3];
-    bool badctrl;
-    STAMP(21);
-    controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    if (A.nctrl && A.sm_in) {  // rollout: computed during the previous step
+#pragma unroll
+      for (int j = 0; j < 3; j++) ctrl[j] = A.nctrl[j * 64 + lane];
+      STAMP(21);
+    } else {
+      const Soa act = soa(A.action, 2, n);
+      const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+      bool badctrl;
+      STAMP(21);
+      controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
+    }
     STAMP(22);
     ScalRows sr;
     scalar_rows(qpos, qvel, sr);  // hinge dofs only: u = qvel there
@@ -2459,6 +2498,15 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
     if (lane == 0) __hip_atomic_store(xflag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     STAMP(14);
   }
+  if (A.next_action && valid) {  // rollout: the next step's controller, off that step's critical path
+    const Soa act = soa(A.next_action, 2, n);
+    const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
+    float c[3];
+    bool badctrl;
+    controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, c, badctrl);
+#pragma unroll
+    for (int j = 0; j < 3; j++) A.nctrl[j * 64 + lane] = c[j];
+  }
   __syncthreads();                                                           // barrier 1
   if (__builtin_amdgcn_ballot_w64(any_redo(sh_bad, lane, 1)) != 0ull) __syncthreads();  // barrier 2
 }
@@ -2506,15 +2554,21 @@ extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_ke
 #endif
 template <int NC, int PW>
 __device__ __forceinline__ void rollout_split(const Args& A) {
-  __shared__ float sm[AK_ROLL_SM ? NSTATE * 64 * PW : 1];
+  __shared__ float sm[2][AK_ROLL_SM ? NSTATE * 64 * PW : 1];
+  __shared__ float nctrl[AK_ROLL_SM && AK_XCH ? 3 * 64 : 1];
 #pragma unroll 1
   for (int k = 0; k < A.ksteps; k++) {
     if (!AK_XCH && k) __syncthreads();
     Args B = step_args(A, k);
     if constexpr (AK_ROLL_SM) {
-      B.sm = sm;
+      B.sm = sm[k & 1];
+      B.sm_next = sm[(k + 1) & 1];
       B.sm_in = k > 0;
       B.sm_out = k + 1 < A.ksteps;
+      if constexpr (AK_XCH) {
+        B.nctrl = nctrl;
+        B.next_action = k + 1 < A.ksteps ? A.action + (size_t)(k + 1) * 2 * A.n : nullptr;
+      }
     }
     step_split<NC, PW>(B);
   }

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 NSTAMP = 24  # AK_NSTAMP of the diagnostic build
+ROLL = int(os.environ.get("STAMPS_ROLLOUT", "1"))  # > 1: stamp the last step of an ackphys_rollout launch of ROLL steps
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
@@ -46,6 +47,7 @@ def main():
     L.ackphys_reset.argtypes = [P, P, C.c_uint64, P, P, P]
     L.ackphys_random_actions.argtypes = [P, P, C.c_int, C.c_uint64, C.c_uint32, P]
     L.ackphys_diag_set_stamps.argtypes = [P]
+    L.ackphys_rollout.argtypes = [P, C.c_int] + [P] * 9 + [C.c_uint32, C.c_uint64, C.c_int, P]
     sys.path.insert(0, REPO)
     from mujoco_playground_amd import _lib
     blob = _lib.load_blob("obstacles" if obst else "flat")
@@ -77,8 +79,12 @@ def main():
         res, spans = [], []
         for k in range(200, 210):
             stamps.zero_()
-            L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags, 0,
-                           stream)
+            if ROLL > 1:  # the stamps left are those of the launch's last step
+                L.ackphys_rollout(ctx, ROLL, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None,
+                                  flags, 0, 0, stream)
+            else:
+                L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, flags,
+                               0, stream)
             torch.cuda.synchronize()
             allv = stamps.cpu().numpy()
             s = allv[: NSTAMP * nb].reshape(NSTAMP, nb)
