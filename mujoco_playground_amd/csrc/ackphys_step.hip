@@ -2618,6 +2618,7 @@ extern "C" __global__ void __launch_bounds__(256) ackphys_actions_kernel(float* 
 #include "../../include/ackphys.h"
 #include "../../include/ackphys_model.h"
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 struct ackphys_ctx {
@@ -2786,6 +2787,23 @@ int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* st
   return launch_steps(ctx, a, flags, stream);
 }
 
+// Envs per quad wave. Per-step launches: 16 (a step lasts as long as the slowest wave, and more
+// waves with fewer envs measured slower). Rollout launches of the flat scene: 8, i.e. 512
+// workgroups, two per CU (55 KB of LDS each), all four SIMDs busy, and each wave's per-step Newton
+// maximum taken over 8 envs instead of 16: 39.6 -> 37.2 us per contacts-on step
+// (tools/quad_epw_sweep.sh). The obstacle kernel's 94 KB of LDS allow one workgroup per CU, so
+// it keeps 16 (8 measured 84 us). ACKPHYS_QUAD_EPW overrides the rollout value (experiments).
+static int quad_epw(bool multi, int scene) {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("ACKPHYS_QUAD_EPW");
+    v = s ? atoi(s) : 0;
+    if (v < 0 || v > 16) v = 0;
+  }
+  if (!multi) return 16;
+  return v ? v : (scene == 0 ? 8 : 16);
+}
+
 static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream) {
   hipError_t e;
   const bool multi = a.ksteps > 1;
@@ -2796,14 +2814,16 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
   if (ctx->scene == 1) {  // the obstacle scene is specialised on the quad mapping only
     if (ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
       return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
-    int blocks = (ctx->n_env + 15) / 16;
+    a.epw = (flags & ACKPHYS_POSTSTEP_OBS) ? 16 : quad_epw(multi, ctx->scene);
+    int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_obst_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(multi ? ackphys_rollout_obst_kernel : ackphys_step_obst_kernel, dim3(blocks), dim3(128), 0,
                          (hipStream_t)stream, a);
   } else if (quad) {
-    int blocks = (ctx->n_env + 15) / 16;
+    a.epw = (flags & ACKPHYS_POSTSTEP_OBS) ? 16 : quad_epw(multi, ctx->scene);
+    int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_quad_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
