@@ -140,14 +140,15 @@ class BatchedAckermannSim:
             # terminal obs rows are written only for done envs: zero-filled like the sim's buffer
             tobs = torch.zeros(k, NOBS, self.n, dtype=f32, device=d) if term_on else None
             info = torch.empty(k, 4, self.n, dtype=f32, device=d) if want_info else None
-        else:
+            ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(tobs), _ptr(info))
+        else:  # the sim's own buffers: their C pointers are prebuilt (one ctypes call, as in step)
             obs, rew, term, trunc = self.obs_soa, self.reward, self.term, self.trunc
-            tobs = self.terminal_obs_soa if term_on else None
-            info = self.info if want_info else None
+            c = self._c
+            ptrs = (c["obs_soa"], c["reward"], c["term"], c["trunc"], c["terminal_obs_soa"] if term_on else None,
+                    c["info"] if want_info else None)
         rc = _lib.lib().ackphys_rollout(
-            self._ctx, k, actions.data_ptr(), self._c["state"], _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
-            _ptr(tobs), _ptr(info), self._c["episode"] if track_episodes else None, flags, self.seed, int(per_step_outputs),
-            _raw_stream(self._dev_index))
+            self._ctx, k, actions.data_ptr(), self._c["state"], *ptrs, self._c["episode"] if track_episodes else None,
+            flags, self.seed, 1 if per_step_outputs else 0, _raw_stream(self._dev_index))
         if rc:
             _lib.check(rc, "ackphys_rollout")
         if per_step_outputs:

@@ -99,3 +99,17 @@ def test_create_rejects_wrong_blob():
     assert rc == -2 and b"specialised" in L.ackphys_last_error()
     rc = L.ackphys_create(b"\0" * 8, 8, 16, 0, C.byref(ctx))
     assert rc == -2
+
+
+def test_rollout_rejects_bad_arguments_without_touching_the_gpu():
+    """ackphys_rollout validates its arguments before any HIP call (EINVAL + message)."""
+    L = _lib.lib()
+    P = C.c_void_p
+    dummy = P(16)  # never dereferenced: every call below fails validation first
+    rc = L.ackphys_rollout(None, 4, dummy, dummy, dummy, dummy, dummy, dummy, None, None, None, 0, 0, 0, None)
+    assert rc == -1 and b"NULL" in L.ackphys_last_error()
+    # a fake (non-NULL) context is only ever compared, never followed, before k_steps is checked
+    rc = L.ackphys_rollout(dummy, 0, dummy, dummy, dummy, dummy, dummy, dummy, None, None, None, 0, 0, 0, None)
+    assert rc == -1 and b"k_steps" in L.ackphys_last_error()
+    rc = L.ackphys_rollout(dummy, 3, None, dummy, dummy, dummy, dummy, dummy, None, None, None, 0, 0, 0, None)
+    assert rc == -1 and b"NULL" in L.ackphys_last_error()
