@@ -2788,11 +2788,12 @@ int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* st
 }
 
 // Envs per quad wave. Per-step launches: 16 (a step lasts as long as the slowest wave, and more
-// waves with fewer envs measured slower). Rollout launches of the flat scene: 8, i.e. 512
-// workgroups, two per CU (55 KB of LDS each), all four SIMDs busy, and each wave's per-step Newton
-// maximum taken over 8 envs instead of 16: 39.6 -> 37.2 us per contacts-on step
-// (tools/quad_epw_sweep.sh). The obstacle kernel's 94 KB of LDS allow one workgroup per CU, so
-// it keeps 16 (8 measured 84 us). ACKPHYS_QUAD_EPW overrides the rollout value (experiments).
+// waves with fewer envs measured slower). Rollout launches: 8, i.e. 512 workgroups, two or more
+// per CU, all four SIMDs busy, and each wave's per-step Newton maximum taken over 8 envs instead
+// of 16: contacts on 39.6 -> 37.2 us per step (tools/quad_epw_sweep.sh). The obstacle scene's
+// slot LDS (94 KB at a 64-lane stride) allows one workgroup per CU, so its 8-env rollout kernel
+// lays the slots out at a 32-lane stride (47 KB; ackphys_rollout_obst8_kernel); at 16 envs per
+// wave and 94 KB, 8 envs had measured 84 us. ACKPHYS_QUAD_EPW overrides (experiments).
 static int quad_epw(bool multi, int scene) {
   static int v = -1;
   if (v < 0) {
@@ -2801,7 +2802,7 @@ static int quad_epw(bool multi, int scene) {
     if (v < 0 || v > 16) v = 0;
   }
   if (!multi) return 16;
-  return v ? v : (scene == 0 ? 8 : 16);
+  return v ? v : 8;
 }
 
 static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream) {
@@ -2819,8 +2820,9 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_obst_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(multi ? ackphys_rollout_obst_kernel : ackphys_step_obst_kernel, dim3(blocks), dim3(128), 0,
-                         (hipStream_t)stream, a);
+      hipLaunchKernelGGL(!multi ? ackphys_step_obst_kernel
+                                : (a.epw <= 8 ? ackphys_rollout_obst8_kernel : ackphys_rollout_obst_kernel),
+                         dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   } else if (quad) {
     a.epw = (flags & ACKPHYS_POSTSTEP_OBS) ? 16 : quad_epw(multi, ctx->scene);
     int blocks = (ctx->n_env + a.epw - 1) / a.epw;
