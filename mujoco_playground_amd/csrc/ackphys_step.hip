@@ -1330,13 +1330,14 @@ __device__ __forceinline__ void xch_get(const float* x, int slot, int stride, Sc
 // The implicit-Euler factor chol(M + h diag(damping)) depends on the steer angles alone (M is
 // constant but for the front spin axes), so the prep wave computes it beside the solve and hands
 // its structural nonzeros over (float4 per lane: 16-byte LDS reads, conflict-free).
-constexpr int eu_words() {
+constexpr int eu_words(int kind = LANE_K(0)) {
   int n = 0;
   for (int i = 0; i < NV; i++)
-    for (int j = 0; j <= i; j++) n += LPAT[LANE_K(0)].nz[i][j] ? 1 : 0;
+    for (int j = 0; j <= i; j++) n += LPAT[kind].nz[i][j] ? 1 : 0;
   return n;
 }
 constexpr int EU_VEC = (eu_words() + 3) / 4;
+constexpr int XH_VEC = (eu_words(LANE_K(1)) + 3) / 4;  // the typical piece's factor (XH)
 // chol(M) (EU = false: qacc_smooth) or chol(M + h diag(damping)) (EU: implicit Euler) at the
 // front steer angles d2, d3
 template <bool EU>
@@ -1358,25 +1359,27 @@ __device__ __forceinline__ void mass_factor(float d2, float d3, float L[NV][NV])
 __device__ __forceinline__ void euler_factor(const float qpos[13], float L[NV][NV]) {
   mass_factor<true>(qpos[W_STEER_QPOS[2]], qpos[W_STEER_QPOS[3]], L);
 }
+template <int KIND = LANE_K(0), int NVEC = EU_VEC>
 __device__ __forceinline__ void eu_put(float* x, int lane, const float L[NV][NV]) {
-  float w[4 * EU_VEC];
+  float w[4 * NVEC];
   int n = 0;
 #pragma unroll
   for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++)
-      if (LPAT[LANE_K(0)].nz[i][j]) w[n++] = AK_F(L, i, j);
+      if (LPAT[KIND].nz[i][j]) w[n++] = AK_F(L, i, j);
 #pragma unroll
-  for (int k = n; k < 4 * EU_VEC; k++) w[k] = 0.0f;
+  for (int k = n; k < 4 * NVEC; k++) w[k] = 0.0f;
   float4* x4 = reinterpret_cast<float4*>(x);
 #pragma unroll
-  for (int v = 0; v < EU_VEC; v++) x4[v * 64 + lane] = make_float4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
+  for (int v = 0; v < NVEC; v++) x4[v * 64 + lane] = make_float4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
 }
+template <int KIND = LANE_K(0), int NVEC = EU_VEC>
 __device__ __forceinline__ void eu_get(const float* x, int lane, float L[NV][NV]) {
-  float w[4 * EU_VEC];
+  float w[4 * NVEC];
   const float4* x4 = reinterpret_cast<const float4*>(x);
 #pragma unroll
-  for (int v = 0; v < EU_VEC; v++) {
+  for (int v = 0; v < NVEC; v++) {
     const float4 t = x4[v * 64 + lane];
     w[4 * v] = t.x; w[4 * v + 1] = t.y; w[4 * v + 2] = t.z; w[4 * v + 3] = t.w;
   }
@@ -1385,7 +1388,49 @@ __device__ __forceinline__ void eu_get(const float* x, int lane, float L[NV][NV]
   for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++)
-      if (LPAT[LANE_K(0)].nz[i][j]) AK_F(L, i, j) = w[n++];
+      if (LPAT[KIND].nz[i][j]) AK_F(L, i, j) = w[n++];
+}
+
+// Contacts-off kernel, typical predicted piece (AK_XH): the quadratic rows of the predicted piece
+// are, in ~99.8 % of env-steps, the steering equality and the friction-loss rows of the two
+// free-rolling front spins (tools/probes/active_set_probe.py). The piece's Hessian
+// H = M + sum over those rows of D J^T J depends on the steer angles and the rows' D alone, so the
+// prep wave builds and factors it beside the dynamics wave (same arithmetic, same order as
+// dyn_post's build); a wave whose lanes all predicted exactly that set takes the factor from LDS.
+constexpr uint32_t xh_rows() {
+  uint32_t m = 1u;  // row 0: the joint equality
+  for (int w = 2; w < 4; w++) m |= 1u << (W_SPIN_DOF[w] - 5);  // front-spin friction-loss rows
+  return m;
+}
+constexpr uint32_t XH_ROWS = xh_rows();
+// the rows of the typical piece that exist for this env (inactive rows add nothing to H)
+__device__ __forceinline__ uint32_t xh_mask(const bool sact[NSCAL]) {
+  uint32_t m = 0u;
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++)
+    if (((XH_ROWS >> r) & 1u) && sact[r]) m |= 1u << r;
+  return m;
+}
+// H of the piece whose quadratic rows are qmask, lower triangle, as dyn_post builds it
+__device__ __forceinline__ void piece_hessian(const float M[NV][NV], uint32_t qmask, const float sD[NSCAL], float eqc2,
+                                              float H[NV][NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; i++)
+#pragma unroll
+    for (int j = 0; j < NV; j++) H[i][j] = (j <= i) ? M[i][j] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < NSCAL; r++) {
+    if (!((qmask >> r) & 1u)) continue;
+    int d1, d2;
+    float c1;
+    scal_dofs(r, d1, c1, d2);
+    H[d1][d1] += sD[r] * c1 * c1;
+    if (d2 >= 0) {
+      H[d2][d2] += sD[r] * eqc2 * eqc2;
+      if (d2 > d1) H[d2][d1] += sD[r] * c1 * eqc2;
+      else H[d1][d2] += sD[r] * c1 * eqc2;
+    }
+  }
 }
 // where the dynamics wave finds the prep wave's Euler factor (XEU): LDS words, flag, lane
 struct EuHand {
@@ -1420,11 +1465,12 @@ __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV],
 
 // forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
 // XEU / XM: the Euler / mass-matrix factor comes from another wave (eh / mh), see step_split
-template <int NC, bool XEU = false, bool XM = false>  // NC = 1: compiled for contacts off (<flag contact="disable"/>)
+// XH: the typical predicted piece's factor comes from the prep wave (hh) for lanes with hok
+template <int NC, bool XEU = false, bool XM = false, bool XH = false>  // NC = 1: contacts off (<flag contact="disable"/>)
 __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
                                          const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
                                          const ScalRows& sr, StepResult& out, EuHand eh = EuHand{},
-                                         EuHand mh = EuHand{}) {
+                                         EuHand mh = EuHand{}, EuHand hh = EuHand{}, bool hok = false) {
   float(&sa)[2][3] = P.sa;
   float(&cyl)[2][3] = P.cyl;
   Solver& sv = P.sv;
@@ -1650,12 +1696,9 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
 #pragma unroll
     for (int r = 0; r < NSCAL; r++) sj[r] = scal_J_dot(r, a) - sj[r];
     float H[NV][NV], grad[NV];
+    uint32_t qmask = 0u;  // the piece's quadratic rows
 #pragma unroll
-    for (int i = 0; i < NV; i++) {
-      grad[i] = 0.0f;
-#pragma unroll
-      for (int j = 0; j < NV; j++) H[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
-    }
+    for (int i = 0; i < NV; i++) grad[i] = 0.0f;
 #pragma unroll
     for (int r = 0; r < NSCAL; r++) {
       if (!sact[r]) continue;
@@ -1666,16 +1709,17 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
       const float f = quad ? -sD[r] * sj[r] : (r <= 6 ? -(float)pst[r] * sfl[r] : 0.0f);
       grad[d1] -= f * c1;
       if (d2 >= 0) grad[d2] -= f * eqc2;
-      if (quad) {
-        H[d1][d1] += sD[r] * c1 * c1;
-        if (d2 >= 0) {
-          H[d2][d2] += sD[r] * eqc2 * eqc2;
-          if (d2 > d1) H[d2][d1] += sD[r] * c1 * eqc2;
-          else H[d1][d2] += sD[r] * c1 * eqc2;
-        }
-      }
+      if (quad) qmask |= 1u << r;
     }
-    chol_sp<LANE_K(1)>(H);
+    // the typical piece (every lane of the wave): factored by the prep wave (AK_XH)
+    const bool typ = XH && hok && qmask == xh_mask(sact);
+    if (XH && __builtin_amdgcn_ballot_w64(!typ) == 0ull) {
+      while (__hip_atomic_load(hh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+      eu_get<LANE_K(1), XH_VEC>(hh.x, hh.lane, H);
+    } else {
+      piece_hessian(sv.M, qmask, sD, eqc2, H);
+      chol_sp<LANE_K(1)>(H);
+    }
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
@@ -2141,10 +2185,18 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 #ifndef AK_XM
 #define AK_XM 1  // with AK_XCH: the observation wave factors M (qacc_smooth) before its observation
 #endif
+#ifndef AK_XH
+// with AK_XCH, contacts off: the prep wave factors the typical predicted piece (xh_rows). Measured
+// off (tools/variant_sweep.sh, rollout, 1000 steps): the dynamics wave gains ~300 cycles but the
+// prep wave's ~1.3k-cycle factorisation delays its rays past the observation wave's, which then
+// holds barrier 1: 4.52 -> 4.97 us per step (prep rays 10-39), 4.79 (10-31), 4.92 (10-27)
+#define AK_XH 0
+#endif
 static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU && !AK_XM), "the hand-overs need the prep wave's exchange");
 constexpr int XEU_OFF = (XCH_WORDS + 1) * 64;  // float offset of the Euler factor words in xch
 constexpr int XM_OFF = XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0);  // ... and of the mass-matrix factor
-constexpr int XCH_FLOATS = XM_OFF + (AK_XM ? 4 * EU_VEC * 64 : 0);
+constexpr int XH_OFF = XM_OFF + (AK_XM ? 4 * EU_VEC * 64 : 0);  // ... and of the typical piece's factor
+constexpr int XCH_FLOATS = XH_OFF + (AK_XH ? 4 * XH_VEC * 64 : 0);
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
@@ -2161,7 +2213,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
   if constexpr (AK_XCH) {
-    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; }
+    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; xflag[4] = 0; }
     __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   }
   const int sms = 64 * npair;  // word stride of the LDS state mirrors
@@ -2231,8 +2283,10 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   }
   if (valid) {
     StepResult res;
-    dyn_post<NC, AK_XEU != 0, AK_XM != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
-                                          EuHand{xch + XEU_OFF, xflag + 2, lane}, EuHand{xch + XM_OFF, xflag + 3, lane});
+    dyn_post<NC, AK_XEU != 0, AK_XM != 0, NC && AK_XH>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
+                                                       EuHand{xch + XEU_OFF, xflag + 2, lane},
+                                                       EuHand{xch + XM_OFF, xflag + 3, lane},
+                                                       EuHand{xch + XH_OFF, xflag + 4, lane}, !bad_state);
     if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
       bad_state = redo = true;
       reset_to_qpos0(qpos, qvel, warm, ctrl);
@@ -2411,6 +2465,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
 // observation wave must not wait for it). Then (AK_XEU) the implicit-Euler factor, which the
 // dynamics wave needs only after its solve (flag 2), and (AK_PREP_RAYS) rangefinders for the
 // observation wave (flag 1); the wave joins barriers 1 and 2 and exits.
+template <int NC>
 __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad, int lane,
                                                int e, bool valid) {
   STAMP_SCOPE
@@ -2420,6 +2475,7 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
   const Soa st = soa(A.state, NSTATE, n);
   float qpos[13];
   bool bad = false;
+  ScalRows sr;
   if (valid) {
     float qvel[NV];
     if (A.sm_in) {  // rollout: LDS state mirror (one wave pair)
@@ -2447,7 +2503,6 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
       controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
     }
     STAMP(22);
-    ScalRows sr;
     scalar_rows(qpos, qvel, sr);  // hinge dofs only: u = qvel there
     STAMP(23);
     xch_put(xch, lane, 64, sr, ctrl);
@@ -2463,6 +2518,24 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
   if (valid && bad) {
 #pragma unroll
     for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
+  }
+  if constexpr (NC && AK_XH) {  // the typical predicted piece's factor (flag 4; unused by reset lanes)
+    if (valid) {
+      float sa[2][3];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; s2++) {
+        float c, sn;
+        fsincos(qpos[W_STEER_QPOS[2 + s2]], sn, c);
+        rot_axis(sa[s2], S_AXIS[s2], W_SPIN_AXIS[2 + s2], c, sn);
+      }
+      float M[NV][NV], H[NV][NV];
+      build_M(M, sa);
+      piece_hessian(M, xh_mask(sr.act), sr.D, sr.eqc2, H);
+      chol_sp<LANE_K(1)>(H);
+      eu_put<LANE_K(1), XH_VEC>(xch + XH_OFF, lane, H);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(xflag + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if constexpr (AK_XEU) {
     if (valid) {
@@ -2519,7 +2592,7 @@ __device__ __forceinline__ void step_split(const Args& A) {
   static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
   __shared__ __attribute__((aligned(16))) float xch[AK_XCH ? XCH_FLOATS : 1];
-  __shared__ int xflag[4];
+  __shared__ int xflag[5];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -2528,7 +2601,7 @@ __device__ __forceinline__ void step_split(const Args& A) {
   const bool valid = lane < A.epw && e < A.n;
   if (wave < PW) step_dyn_wave<NC>(A, lds, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
   else if (wave < 2 * PW) step_obs_wave(A, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
-  else step_prep_wave(A, xch, xflag, sh_bad, lane, blockIdx.x * A.epw + lane, lane < A.epw && blockIdx.x * A.epw + lane < A.n);
+  else step_prep_wave<NC>(A, xch, xflag, sh_bad, lane, blockIdx.x * A.epw + lane, lane < A.epw && blockIdx.x * A.epw + lane < A.n);
 }
 #ifndef AK_NC_PW
 #define AK_NC_PW 1  // wave pairs per workgroup of the contacts-off kernel
