@@ -1444,6 +1444,7 @@ struct DynPre {
   float sa[2][3], cyl[2][3];
   Solver sv;  // M; fs = -bias - damping (actuator forces added in dyn_post)
 };
+template <bool BIAS = true>  // BIAS = false: fs (bias + passive) comes from the observation wave (AK_XB)
 __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV], const float R[9], DynPre& P) {
   // front steer angles -> spin / cylinder axes in the chassis frame
 #pragma unroll
@@ -1456,31 +1457,39 @@ __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV],
   }
   STAMP(2);
   build_M(P.sv.M, P.sa);
-  float b[NV];
-  bias(u, R, P.sa, b);
-  // passive damping (mj_passive)
+  if constexpr (BIAS) {
+    float b[NV];
+    bias(u, R, P.sa, b);
+    // passive damping (mj_passive)
 #pragma unroll
-  for (int i = 0; i < NV; i++) P.sv.fs[i] = -b[i] - DAMPING[i] * u[i];
+    for (int i = 0; i < NV; i++) P.sv.fs[i] = -b[i] - DAMPING[i] * u[i];
+  }
 }
 
 // forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
 // XEU / XM: the Euler / mass-matrix factor comes from another wave (eh / mh), see step_split
 // XH: the typical predicted piece's factor comes from the prep wave (hh) for lanes with hok
-template <int NC, bool XEU = false, bool XM = false, bool XH = false>  // NC = 1: contacts off (<flag contact="disable"/>)
+// XB (with XM): fs = -bias - damping u comes with the mass-matrix factor, at fsx[i * 64]
+template <int NC, bool XEU = false, bool XM = false, bool XH = false, bool XB = false>  // NC = 1: contacts off
 __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
                                          const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
                                          const ScalRows& sr, StepResult& out, EuHand eh = EuHand{},
-                                         EuHand mh = EuHand{}, EuHand hh = EuHand{}, bool hok = false) {
+                                         EuHand mh = EuHand{}, EuHand hh = EuHand{}, bool hok = false,
+                                         const float* fsx = nullptr) {
+  static_assert(!XB || XM, "fs is handed over with the mass-matrix factor");
   float(&sa)[2][3] = P.sa;
   float(&cyl)[2][3] = P.cyl;
   Solver& sv = P.sv;
   (void)sa;
+  float fact[3];  // XB: actuator forces, added once fs has arrived
+  (void)fact;
   {  // actuators (mj_fwdActuation)
     float c0 = ctrl[0];
     if (ACT_CTRLLIMITED[0]) c0 = fminf(fmaxf(c0, ACT_CTRLRANGE[0][0]), ACT_CTRLRANGE[0][1]);
     float f0 = ACT_GAIN[0] * c0 + ACT_BIAS1[0] * qpos[ACT_STEER_QPOS] + ACT_BIAS2[0] * u[ACT_STEER_DOF];
     if (ACT_FORCELIMITED[0]) f0 = fminf(fmaxf(f0, ACT_FORCERANGE[0][0]), ACT_FORCERANGE[0][1]);
-    sv.fs[ACT_STEER_DOF] += f0;
+    if constexpr (!XB) sv.fs[ACT_STEER_DOF] += f0;
+    else fact[0] = f0;
     float c1 = ctrl[1], c2 = ctrl[2];
     if (ACT_CTRLLIMITED[1]) c1 = fminf(fmaxf(c1, ACT_CTRLRANGE[1][0]), ACT_CTRLRANGE[1][1]);
     if (ACT_CTRLLIMITED[2]) c2 = fminf(fmaxf(c2, ACT_CTRLRANGE[2][0]), ACT_CTRLRANGE[2][1]);
@@ -1488,14 +1497,26 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     float f2 = ACT_GAIN[2] * c2 + ACT_BIAS2[2] * u[ACT_RR_DOF];
     if (ACT_FORCELIMITED[1]) f1 = fminf(fmaxf(f1, ACT_FORCERANGE[1][0]), ACT_FORCERANGE[1][1]);
     if (ACT_FORCELIMITED[2]) f2 = fminf(fmaxf(f2, ACT_FORCERANGE[2][0]), ACT_FORCERANGE[2][1]);
-    sv.fs[ACT_RL_DOF] += f1;
-    sv.fs[ACT_RR_DOF] += f2;
+    if constexpr (!XB) {
+      sv.fs[ACT_RL_DOF] += f1;
+      sv.fs[ACT_RR_DOF] += f2;
+    } else {
+      fact[1] = f1;
+      fact[2] = f2;
+    }
   }
   // qacc_smooth = M^-1 fs
   float L[NV][NV];
   if constexpr (XM) {  // factored by the observation wave (same steer angles)
     while (__hip_atomic_load(mh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
     eu_get(mh.x, mh.lane, L);
+    if constexpr (XB) {  // bias + passive from the observation wave, then the actuator forces as above
+#pragma unroll
+      for (int i = 0; i < NV; i++) sv.fs[i] = fsx[i * 64];
+      sv.fs[ACT_STEER_DOF] += fact[0];
+      sv.fs[ACT_RL_DOF] += fact[1];
+      sv.fs[ACT_RR_DOF] += fact[2];
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < NV; i++)
@@ -2192,11 +2213,19 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
 // holds barrier 1: 4.52 -> 4.97 us per step (prep rays 10-39), 4.79 (10-31), 4.92 (10-27)
 #define AK_XH 0
 #endif
+#ifndef AK_XB
+// with AK_XM: the observation wave also computes fs = -bias - damping u (off the dynamics wave).
+// Measured off (tools/variant_sweep.sh, rollout, 1000 steps): 4.52 -> 5.03 us per contacts-off
+// step -- the observation wave's factor + bias arrive later than the dynamics wave's own bias
+#define AK_XB 0
+#endif
+static_assert(!AK_XB || AK_XM, "AK_XB hands fs over with the mass-matrix factor");
 static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU && !AK_XM), "the hand-overs need the prep wave's exchange");
 constexpr int XEU_OFF = (XCH_WORDS + 1) * 64;  // float offset of the Euler factor words in xch
 constexpr int XM_OFF = XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0);  // ... and of the mass-matrix factor
 constexpr int XH_OFF = XM_OFF + (AK_XM ? 4 * EU_VEC * 64 : 0);  // ... and of the typical piece's factor
-constexpr int XCH_FLOATS = XH_OFF + (AK_XH ? 4 * XH_VEC * 64 : 0);
+constexpr int XB_OFF = XH_OFF + (AK_XH ? 4 * XH_VEC * 64 : 0);  // ... and of fs (AK_XB)
+constexpr int XCH_FLOATS = XB_OFF + (AK_XB ? NV * 64 : 0);
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
@@ -2263,7 +2292,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
     if (bad_state) reset_to_qpos0(qpos, qvel, warm, ctrl);  // mj_checkPos / mj_checkVel -> mj_resetData
     to_u(qpos, qvel, warm, R, u, wu);
-    dyn_pre(qpos, u, R, P);
+    dyn_pre<!(AK_XCH && AK_XB)>(qpos, u, R, P);
   }
   ScalRows sr;
   if constexpr (AK_XCH) {
@@ -2283,10 +2312,11 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   }
   if (valid) {
     StepResult res;
-    dyn_post<NC, AK_XEU != 0, AK_XM != 0, NC && AK_XH>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
-                                                       EuHand{xch + XEU_OFF, xflag + 2, lane},
-                                                       EuHand{xch + XM_OFF, xflag + 3, lane},
-                                                       EuHand{xch + XH_OFF, xflag + 4, lane}, !bad_state);
+    dyn_post<NC, AK_XEU != 0, AK_XM != 0, NC && AK_XH, AK_XB != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
+                                                                  EuHand{xch + XEU_OFF, xflag + 2, lane},
+                                                                  EuHand{xch + XM_OFF, xflag + 3, lane},
+                                                                  EuHand{xch + XH_OFF, xflag + 4, lane}, !bad_state,
+                                                                  xch + XB_OFF + lane);
     if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
       bad_state = redo = true;
       reset_to_qpos0(qpos, qvel, warm, ctrl);
@@ -2346,9 +2376,9 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
   bool bad_state = false;
   float ep0 = 0.0f, ep1 = 0.0f, ep2 = 0.0f, ep3 = 0.0f;
   const Soa ep = soa(A.ep, 4, n);
+  float qvel[NV];
   if (valid) {
     // rollout steps after a launch's first read the LDS state mirror instead (same words)
-    float qvel[NV];
     if (A.sm_in) {
       const float* smr = A.sm + slot;
       const int sms = 64 * npair;
@@ -2385,6 +2415,23 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
       mass_factor<false>(bad_state ? QPOS0[W_STEER_QPOS[2]] : qpos[W_STEER_QPOS[2]],
                          bad_state ? QPOS0[W_STEER_QPOS[3]] : qpos[W_STEER_QPOS[3]], L);
       eu_put(xch + XM_OFF, lane, L);
+      if constexpr (AK_XB) {  // fs = -bias - damping u of the (reset) state, as dyn_pre computes it
+        float qp[13], qv[NV], wz[NV], R[9], u[NV], wu[NV], sa[2][3], b[NV];
+#pragma unroll
+        for (int i = 0; i < 13; i++) qp[i] = bad_state ? QPOS0[i] : qpos[i];
+#pragma unroll
+        for (int i = 0; i < NV; i++) { qv[i] = bad_state ? 0.0f : qvel[i]; wz[i] = 0.0f; }
+        to_u(qp, qv, wz, R, u, wu);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+          float c, sn;
+          fsincos(qp[W_STEER_QPOS[2 + s2]], sn, c);
+          rot_axis(sa[s2], S_AXIS[s2], W_SPIN_AXIS[2 + s2], c, sn);
+        }
+        bias(u, R, sa, b);
+#pragma unroll
+        for (int i = 0; i < NV; i++) xch[XB_OFF + i * 64 + lane] = -b[i] - DAMPING[i] * u[i];
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(xflag + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
