@@ -17,9 +17,9 @@ DEV = "cuda:0"
 CASES = [  # (scene, contacts, variant, poststep)
     ("flat", False, "auto", False),    # BASELINE configs[1]: ackphys_rollout_nc_kernel
     ("flat", False, "lane16", False),  # 16 envs per wave
-    ("flat", True, "auto", False),     # configs[2]: ackphys_rollout_quad_kernel
+    ("flat", True, "auto", False),     # configs[2]: ackphys_rollout_quad_kernel (8 envs per wave)
     ("flat", True, "lane", False),     # ackphys_rollout_kernel (lane mapping with contacts)
-    ("obstacles", True, "auto", False),  # configs[4]: ackphys_rollout_obst_kernel
+    ("obstacles", True, "auto", False),  # configs[4]: ackphys_rollout_obst8_kernel (8 envs per wave)
     ("flat", True, "auto", True),      # post-step obs: K single-step launches
 ]
 
@@ -101,3 +101,26 @@ def test_rollout_rejects_bad_shapes():
         s.rollout(torch.zeros(64, 2, device=DEV))
     with pytest.raises(ValueError):
         s.rollout(torch.zeros(0, 64, 2, device=DEV))
+
+
+@pytest.mark.parametrize("scene,contacts", [("flat", False), ("flat", True), ("obstacles", True)])
+def test_rollout_full_episode_4096(scene, contacts):
+    """BASELINE sizes: 4096 envs through a whole episode (truncation at step 1000 inside the launch):
+    the rollout's final state, episode statistics and every step's reward / flags are bit-identical
+    to 1001 ackphys_step calls; the truncation step resets every env exactly once."""
+    n, K = 4096, 1001
+    a, b = _pair(n, scene, contacts, "auto", False, eplen=1000)
+    acts = a.random_actions(K, seed=4)
+    obs, rew, term, trunc = a.rollout(acts, want_info=False, want_terminal=False)
+    rb = torch.empty(K, n, device=DEV)
+    tb = torch.empty(K, n, dtype=torch.uint8, device=DEV)
+    for k in range(K):
+        _, r, t, tr = b.step(acts[k], want_info=False, want_terminal=False)
+        rb[k] = r
+        tb[k] = t | (tr << 1)
+    assert torch.equal(rew, rb)
+    assert torch.equal(term | (trunc << 1), tb)
+    assert torch.equal(obs[-1], b.obs_soa)
+    assert torch.equal(a.state, b.state)
+    assert torch.equal(a.episode, b.episode)
+    assert int(trunc[999].sum()) == n - int(term[:999].any(0).sum())  # envs not terminated earlier
