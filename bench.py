@@ -17,6 +17,7 @@ under "obstacles" (env steps, contacts on) and its PPO rollout under "obstacles.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -79,10 +80,12 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
         sim.state.copy_(snap[0])  # capture launches nothing, but restore anyway
         sim.episode.copy_(snap[1])
     stream = torch.cuda.current_stream(device)
+    launch = None if (per_step or g is not None) else sim.rollout_launcher(timed_actions)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
     shard.barrier(world, device)
     torch.cuda.synchronize(device)
+    gc.disable()  # no collector pass inside the host-clocked window
     t0 = time.perf_counter()
     ev0.record(stream)
     if g is not None:
@@ -91,16 +94,28 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
         for k in range(steps):
             sim.step(step_actions[k], want_info=False)
     else:
-        sim.rollout(timed_actions, want_info=False, per_step_outputs=False)
+        launch()
     ev1.record(stream)
     gathered = shard.gather_episode_stats(sim.episode, world)  # the per-rollout RCCL exchange
     torch.cuda.synchronize(device)
     shard.barrier(world, device)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
+    gc.enable()
     elapsed = shard.max_over_ranks(t1 - t0, world, device)
     kern_ms = ev0.elapsed_time(ev1) / steps
     return sim, elapsed, kern_ms, shard.summarize_returns(gathered), actions
+
+
+def clock_warm(device, n_env: int, seconds: float = 0.2):
+    """Untimed GPU work on a throwaway sim until ~`seconds` have passed (clock ramp-up)."""
+    sim = BatchedAckermannSim(n_env, device, seed=1, contacts=False)
+    sim.reset()
+    acts = sim.random_actions(200, seed=1)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        sim.rollout(acts, want_info=False, per_step_outputs=False)
+        torch.cuda.synchronize(device)
 
 
 def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_epochs=10, seed=0, scene="flat"):
@@ -151,6 +166,53 @@ def to_f64_state(st: torch.Tensor) -> np.ndarray:
     return out
 
 
+TOL_QPOS, TOL_QVEL = 1e-5, 1e-3  # tests/test_gpu_parity.py's stated f32 tolerances
+
+
+def parity_sample(o, device, contacts, flags, seed, n, steps, settle=0, drift=True):
+    """Teacher-forced parity on a sample (same flags / seed as the timed run): every step starts the
+    oracle from the GPU's state; max errors and the env-steps over the stated tolerances (contact
+    activation boundaries, DESIGN.md §5, can exceed them; the parity tests excuse and cap those)."""
+    sim = BatchedAckermannSim(n, device, seed=seed, contacts=contacts)
+    sim.reset()
+    acts = sim.random_actions(settle + steps, seed=seed)
+    if settle:
+        sim.rollout(acts[:settle], want_info=False, per_step_outputs=False)
+    eq = ev = eo = 0.0
+    over = 0
+    for k in range(settle, settle + steps):
+        s_before = to_f64_state(sim.state)
+        sim.step(acts[k], want_info=False)
+        torch.cuda.synchronize(device)
+        s_after = to_f64_state(sim.state)
+        oobs, orew, _, _, _, _ = o.step(s_before, acts[k].cpu().numpy(), flags=flags, seed=seed)
+        dq = np.abs(s_after[:, 0:13] - s_before[:, 0:13]).max(1)
+        dv = np.abs(s_after[:, 13:25] - s_before[:, 13:25]).max(1)
+        over += int(((dq > TOL_QPOS) | (dv > TOL_QVEL)).sum())
+        eq, ev = max(eq, float(dq.max())), max(ev, float(dv.max()))
+        eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs).max()))
+    out = {"max_abs_qpos_err": eq, "max_abs_qvel_err": ev, "max_abs_obs_err": eo,
+           "env_steps_over_tolerance": over, "tolerance": {"qpos": TOL_QPOS, "qvel": TOL_QVEL},
+           "sample": f"{n} envs x {steps} teacher-forced steps, contacts {'on' if contacts else 'off'}, "
+                     + (f"after {settle} settle steps" if settle else "from reset") + " (f32 GPU vs f64 oracle)"}
+    if drift:
+        # free-running drift (not gated, SURVEY §8d): GPU and oracle both run their own state from the
+        # same reset under the same actions; max |dqpos| after 1/10/100 steps
+        fsim = BatchedAckermannSim(n, device, seed=seed, contacts=contacts)
+        fsim.reset()
+        facts = fsim.random_actions(100, seed=seed)
+        fst = to_f64_state(fsim.state)
+        d = {}
+        for k in range(100):
+            fsim.step(facts[k], want_info=False)
+            o.step(fst, facts[k].cpu().numpy(), flags=flags, seed=seed)
+            if k + 1 in (1, 10, 100):
+                torch.cuda.synchronize(device)
+                d[str(k + 1)] = float(np.abs(to_f64_state(fsim.state)[:, 0:13] - fst[:, 0:13]).max())
+        out["free_running_qpos_drift"] = d
+    return out
+
+
 def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s=12.0, do_timing=True):
     """Oracle as the checker: teacher-forced max|qpos| error on a sample, and the CPU baseline
     (oracle on the host cores, bounded sample of the same workload)."""
@@ -158,36 +220,10 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
     from oracle.oracle import FLAG_AUTORESET, FLAG_CONTACTS, Oracle
     o = Oracle(_lib.load_blob())
     flags = (FLAG_CONTACTS if contacts else 0) | FLAG_AUTORESET
-    # teacher-forced parity on a sample (same flags / seed as the timed run)
-    sim = BatchedAckermannSim(parity_envs, device, seed=seed, contacts=contacts)
-    sim.reset()
-    acts = sim.random_actions(parity_steps, seed=seed)
-    eq = ev = eo = 0.0
-    for k in range(parity_steps):
-        s_before = to_f64_state(sim.state)
-        sim.step(acts[k], want_info=False)
-        torch.cuda.synchronize(device)
-        s_after = to_f64_state(sim.state)
-        oobs, orew, _, _, _, _ = o.step(s_before, acts[k].cpu().numpy(), flags=flags, seed=seed)
-        eq = max(eq, float(np.abs(s_after[:, 0:13] - s_before[:, 0:13]).max()))
-        ev = max(ev, float(np.abs(s_after[:, 13:25] - s_before[:, 13:25]).max()))
-        eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs).max()))
-    # free-running drift (not gated): GPU and oracle both run their own state from the
-    # same reset under the same actions; max |dqpos| after 1/10/100 steps
-    fsim = BatchedAckermannSim(parity_envs, device, seed=seed, contacts=contacts)
-    fsim.reset()
-    facts = fsim.random_actions(100, seed=seed)
-    fst = to_f64_state(fsim.state)
-    drift = {}
-    for k in range(100):
-        fsim.step(facts[k], want_info=False)
-        o.step(fst, facts[k].cpu().numpy(), flags=flags, seed=seed)
-        if k + 1 in (1, 10, 100):
-            torch.cuda.synchronize(device)
-            drift[str(k + 1)] = float(np.abs(to_f64_state(fsim.state)[:, 0:13] - fst[:, 0:13]).max())
-    parity = {"max_abs_qpos_err": eq, "max_abs_qvel_err": ev, "max_abs_obs_err": eo,
-              "sample": f"{parity_envs} envs x {parity_steps} teacher-forced steps from reset (f32 GPU vs f64 oracle)",
-              "free_running_qpos_drift": drift}
+    parity = parity_sample(o, device, contacts, flags, seed, parity_envs, parity_steps, settle=0)
+    if contacts is False:  # the contacts-on sample too, on ground-contact steps (after the settle steps)
+        parity["contacts_on"] = parity_sample(o, device, True, FLAG_CONTACTS | FLAG_AUTORESET, seed, parity_envs,
+                                              parity_steps, settle=SETTLE_STEPS, drift=False)
     if not do_timing:
         return parity, None
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -233,18 +269,59 @@ def cpu_leg(device, contacts, seed=0, parity_envs=256, parity_steps=20, budget_s
     return parity, base
 
 
-def load_pmc(kern_name: str, contacts: bool):
-    """PMC summary of the kernel from the committed rocprofv3 passes (tools/profile_pmc.py); None if
-    that profile is absent or was taken on another workload."""
-    path = os.path.join(HERE, "profiles", "pmc_latest.json")
+def _profile(name: str):
+    """A committed measurement summary under profiles/ (None if absent)."""
     try:
-        with open(path) as f:
-            k = json.load(f).get(kern_name)
-        if not k or bool(k.get("contacts")) != contacts:
-            return None
-        return k
+        with open(os.path.join(HERE, "profiles", name)) as f:
+            return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def load_pmc(kern_name: str, contacts: bool, steps: int):
+    """PMC summary of the kernel from the committed rocprofv3 passes (tools/profile_pmc.py ->
+    profiles/pmc_latest.json), for the launch length K nearest to `steps` (a launch's first-step
+    loads and last-step stores are spread over its K steps); None if absent. The counters are NOT
+    measured in this run: the returned entry names its source."""
+    d = _profile("pmc_latest.json") or {}
+    cands = [v for v in d.values() if isinstance(v, dict) and v.get("kernel") == kern_name
+             and bool(v.get("contacts")) == contacts]
+    if not cands:
+        return None
+    best = min(cands, key=lambda v: abs(v["launch_steps"] - steps))
+    return dict(best, source=f"profiles/pmc_latest.json ({d.get('_round', '?')}; rocprofv3 --pmc, separate passes, "
+                            f"launch of K={best['launch_steps']} steps{'' if best['launch_steps'] == steps else ', nearest to --steps'})")
+
+
+CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md constants table)
+
+
+def critical_path(kern_name: str, kern_ms: float):
+    """The dynamics wave's dependent chain against the kernel time: cycles per step from the
+    stamped diagnostic build (tools/stamps.py -> profiles/critical_path_latest.json), not this run."""
+    d = _profile("critical_path_latest.json") or {}
+    e = next((v for v in d.values() if isinstance(v, dict) and v.get("kernel") == kern_name), None)
+    if e is None:
+        return None
+    kc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
+    return {"dyn_wave_cycles_per_step": e["dyn_wave_cycles_per_step_median"], "kernel_cycles_per_step": kc,
+            "frac_of_kernel_time": e["dyn_wave_cycles_per_step_median"] / kc, "clock_ghz_assumed": CLOCK_GHZ,
+            "phases_median": e.get("phases_median"),
+            "source": f"profiles/critical_path_latest.json ({d.get('_round', '?')}): {e.get('measured', '')}"}
+
+
+def mfma_summary():
+    """MFMA utilisation of the PPO kernels (tools/profile_mfma.py -> profiles/mfma_latest.json)."""
+    d = _profile("mfma_latest.json")
+    if not d:
+        return None
+    out = {k: {"mfma_util": v.get("mfma_util"), "mfma_tflops": v.get("mfma_tflops"),
+               "peak_tflops": v.get("f32_mfma_peak_tflops"), "duration_us": v.get("median_duration_ns", 0) / 1e3}
+           for k, v in d.items() if isinstance(v, dict) and k.startswith("ackppo")}
+    out["source"] = f"profiles/mfma_latest.json ({d.get('_round', '?')}; rocprofv3 --pmc on tools/ppo_kbench.py)"
+    out["note"] = ("the physics step kernels use no MFMA (per-lane scalar f32 work); the PPO learner's GEMM-shaped "
+                   "layers run v_mfma_f32_16x16x4_f32")
+    return out
 
 
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md constants table (spec)
@@ -266,7 +343,47 @@ def oracle_flops(config_key: str, rate: float):
                     "the kernels execute fewer (structured factorisations, floor-only rays, predicted pieces)"}
 
 
+def launch_command(argv: list, gpus: int, port: int) -> list:
+    """The torchrun command that runs this bench with one rank per GPU (the driver's own N>1 verb:
+    torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(argv: list, gpus: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a torchrun environment: start the N rank
+    processes as children and return their exit status. This process never touches the GPU (no
+    HIP call before the children exist; nothing is exec'ed from a GPU-initialised process); rank 0
+    prints the JSON line on the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between the rank processes)
+    env["ACKPHYS_SPAWNED"] = "1"
+    return subprocess.run(launch_command(argv, gpus, port), env=env).returncode
+
+
+def check_world(gpus: int, world: int, rank: int) -> str:
+    """Each rank refuses a run whose world is not the --gpus it was asked for, or (on a GPU node)
+    a multi-GPU world whose backend is not RCCL ("nccl" on ROCm). The only exception is a
+    rehearsal of N ranks on one device (ACKPHYS_DEVICE_OVERRIDE, tools/rehearse_dist.sh), where
+    RCCL cannot run and gloo stands in. Returns the backend name ("none" at world 1)."""
+    import torch.distributed as dist
+    if world != gpus:
+        raise SystemExit(f"bench.py rank {rank}: world size {world} != --gpus {gpus}")
+    if world == 1:
+        return "none"
+    backend = dist.get_backend()
+    if (torch.cuda.is_available() and backend != "nccl" and os.environ.get("ACKPHYS_DEVICE_OVERRIDE") is None):
+        raise SystemExit(f"bench.py rank {rank}: backend {backend!r} on a GPU node (RCCL 'nccl' required)")
+    return backend
+
+
 def main():
+    argv = sys.argv[1:]
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -281,20 +398,42 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the timed steps' launches as one captured hipGraph")
     ap.add_argument("--per-step", action="store_true",
                     help="time K ackphys_step launches instead of one ackphys_rollout launch of K steps")
+    ap.add_argument("--no-per-step", action="store_true",
+                    help="skip the per-step-launch legs (K ackphys_step launches of the same workloads)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="ranks check the world and backend, print one JSON line and exit (no GPU work)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(argv, a.gpus))  # before any GPU call in this process
     rank, world, local = shard.init()
+    backend = check_world(a.gpus, world, rank)
+    if a.check_launch:
+        ranks = [rank]
+        if world > 1:
+            import torch.distributed as dist
+            got = [None] * world
+            dist.all_gather_object(got, rank)
+            ranks = got
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "n_gpus": world, "ranks": ranks, "backend": backend}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     device = shard.device_for(local)
     torch.cuda.set_device(device)
     contacts = bool(a.contacts)
     fused = not (a.per_step or a.graph)
     total_envs = a.envs * world
-    # leg order: the secondary (other contacts setting) leg runs first, so the headline window
-    # does not start on a GPU that has been idle through the process start (its clocks still low:
-    # a 20-step window right after start-up measured ~15 % slower per step)
     sec_run = None
     if not a.no_secondary:
         sec_run = run_gpu(a.envs, a.steps, a.warmup, not contacts, rank, world, device, variant=a.variant,
                           graph=a.graph, per_step=a.per_step)
+    # the headline window must not start on a GPU whose clocks are still low after an idle spell (a
+    # 20-step window right after start-up measured ~15 % slower per step): ~0.2 s of untimed work on
+    # a throwaway sim first, whatever ran before (so the value does not depend on --no-secondary)
+    clock_warm(device, a.envs)
     sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
                                              variant=a.variant, graph=a.graph, per_step=a.per_step)
     value = total_envs * a.steps / elapsed
@@ -305,12 +444,13 @@ def main():
                                   per_step=True)
         return {"value": total_envs * a.steps / el, "ms_per_step": el * 1e3 / a.steps, "kernel_ms": km,
                 "note": "K ackphys_step launches (one per step) instead of one ackphys_rollout launch"}
-    per_step_launch = per_step_leg(contacts) if fused else None
+    do_per_step = fused and not a.no_per_step
+    per_step_launch = per_step_leg(contacts) if do_per_step else None
     secondary = None
     if sec_run is not None:
         _, el2, km2, _, _ = sec_run
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
-                     "kernel_ms": km2, "per_step_launch": per_step_leg(not contacts) if fused else None,
+                     "kernel_ms": km2, "per_step_launch": per_step_leg(not contacts) if do_per_step else None,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup,
                      "flops": oracle_flops("configs[1] contacts off" if contacts else "configs[2] contacts on",
                                            total_envs * a.steps / el2)}
@@ -322,8 +462,8 @@ def main():
         obstacles = {"workload": f"v2 robot in ackermann_maze_flat.xml (38 static boxes), {a.envs} envs/GPU, "
                                  "random ctrl, contacts enabled, spawn at the scene's free cell",
                      "value": total_envs * a.steps / el3, "unit": "env-steps/s", "ms_per_step": el3 * 1e3 / a.steps,
-                     "kernel": "ackphys_rollout_obst_kernel" if fused else "ackphys_step_obst_kernel", "kernel_ms": km3,
-                     "per_step_launch": per_step_leg(True, "obstacles") if fused else None, "episodes": rets3,
+                     "kernel": "ackphys_rollout_obst8_kernel" if fused else "ackphys_step_obst_kernel", "kernel_ms": km3,
+                     "per_step_launch": per_step_leg(True, "obstacles") if do_per_step else None, "episodes": rets3,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS),
                      "flops": oracle_flops("configs[4] obstacle scene, contacts on", total_envs * a.steps / el3),
                      "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
@@ -334,19 +474,24 @@ def main():
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
     kern = "quad" if (a.variant == "quad" or (a.variant == "auto" and contacts)) else ("" if contacts else "nc")
     kern = ("ackphys_rollout" if fused else "ackphys_step") + (f"_{kern}" if kern else "") + "_kernel"
-    pmc = load_pmc(kern, contacts)
-    traffic = pmc.get("hbm_bytes_per_step") if pmc else None
+    pmc = load_pmc(kern, contacts, a.steps)
     valu = None
     if pmc and pmc.get("valu_insts_per_wave_step"):
         # one wave alone issues a dependent VALU op every ~4 cycles (MI355X_MICROARCH.md constants
         # table; tools/probes/launch_floor.py measures 4.1 cycles per op of a dependent FMA chain)
         valu = {"insts_per_wave_step": pmc["valu_insts_per_wave_step"], "waves": pmc["SQ_WAVES"],
-                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave_step"] * 4 / (kern_ms * 1e-3 * 2.4e9),
+                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave_step"] * 4 / (kern_ms * 1e-3 * CLOCK_GHZ * 1e9),
+                "source": pmc["source"],
                 "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave "
-                        "dependent-op rate (4 cyc/op, 2.4 GHz), per-wave average over the kernel's waves "
-                        "(contacts off: dynamics, observation and prep waves); the rest is dependency/memory "
-                        "latency (and, per ackphys_step launch, the ~2.3 us launch floor of an empty kernel of "
-                        "this grid)"}
+                        "dependent-op rate (4 cyc/op), per-wave average over the kernel's waves (contacts off: "
+                        "dynamics, observation and prep waves); the rest is dependency/memory latency"}
+    hbm = {"nominal_bytes_per_step": bpe * a.envs,
+           "counter_bytes_per_step": pmc.get("hbm_bytes_per_step") if pmc else None,
+           "counter_source": pmc["source"] if pmc else None,
+           "note": ("nominal = the algorithmic 690 B per env-step (state in/out, action, obs, reward, flags, "
+                    "episode stats); counter = FETCH_SIZE x2 + WRITE_SIZE per step of the profiled launch: "
+                    "between steps the state lives in an LDS mirror and in-place outputs stay in L2, so real "
+                    "HBM traffic is far below the nominal figure")}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -356,21 +501,30 @@ def main():
             "config": {"workload": f"ackermann_robot_v2.xml, {a.envs} envs/GPU, random ctrl, contacts "
                                    f"{'enabled' if contacts else 'disabled'} (BASELINE configs[{2 if contacts else 1}])",
                        "envs_per_gpu": a.envs, "total_envs": total_envs, "episode_len": 1000,
-                       "parallelism": f"dp{world} (independent env shards, 1 all_gather of episode stats)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kern, "kernel_ms": kern_ms, "valu": valu,
+                       "parallelism": f"dp{world} (independent env shards, 1 all_gather of episode stats)",
+                       "backend": backend,
+                       "launcher": ("bench.py --gpus N (torch.distributed.run children)" if os.environ.get(
+                           "ACKPHYS_SPAWNED") else ("torchrun" if world > 1 else "single process"))},
+            "roofline": {"bound": "valu-latency", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (pmc["hbm_bytes_per_step"] * a.steps if (pmc and fused) else
+                                     (pmc["hbm_bytes_per_step"] if pmc else None)),
+                         "traffic_unit": "HBM bytes per launch (PMC, profiled separately: see hbm.counter_source)",
+                         "kernel": kern, "kernel_ms": kern_ms,
+                         "critical_path": critical_path(kern, kern_ms), "valu": valu, "hbm": hbm,
+                         "mfma": mfma_summary(),
                          "flops": oracle_flops("configs[2] contacts on" if contacts else "configs[1] contacts off",
                                                value),
                          "algorithmic_bytes_per_env_step": bpe,
-                         "unit_of_work": (f"one step of {a.envs} envs: achieved = {bpe} B x envs / kernel_ms, "
-                                          "traffic = PMC HBM bytes per step (the profiled launch's bytes / its "
-                                          "steps); " + (f"one launch runs all {a.steps} timed steps, so per launch "
-                                                        "both scale by the step count" if fused else
-                                                        "one launch per step")),
-                         "note": "latency/VALU-bound: 4096 envs = 64 dynamics + 64 observation + 64 prep "
-                                 "waves (lane mapping, contacts off), i.e. 192 of 1024 SIMDs; HBM fraction is "
-                                 "tiny by construction"},
+                         "unit_of_work": (f"one step of {a.envs} envs: achieved = {bpe} B x envs / kernel_ms (HBM, "
+                                          "nominal bytes); " + (f"one launch runs all {a.steps} timed steps, so per "
+                                                                "launch bytes and time both scale by the step count"
+                                                                if fused else "one launch per step")),
+                         "note": ("bound = the dynamics wave's dependent f32 VALU chain (critical_path: its cycles "
+                                  "per step are the kernel's); 4096 envs = 64 dynamics + 64 observation + 64 prep "
+                                  "waves (lane mapping, contacts off), 192 of 1024 SIMDs. achieved/peak/frac are "
+                                  "the HBM figures the contract asks for, nominal bytes over kernel time: HBM is "
+                                  "not what limits this kernel")},
             "timing": ("one ackphys_rollout launch of the K timed steps (pre-drawn actions resident in HBM; every "
                        "step computed and its outputs written)" if fused else
                        ("K ackphys_step launches replayed from a hipGraph" if a.graph else

@@ -62,17 +62,25 @@ class EnvParams(C.Structure):
 
 
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:
-    if not force and os.path.exists(out):
-        t = os.path.getmtime(out)
-        if all(os.path.getmtime(s) <= t for s in sources):
-            return out
-    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, *HIPCC_FLAGS, *extra, "-o", out + ".tmp", sources[0]]
+    # the compile command is part of the up-to-date check: a flag-only change rebuilds (a stale
+    # library would silently skew kernel timings and register counts)
+    stamp = out + ".cmd"
+    cmd_text = " ".join(cmd) + "\n"
+    if not force and os.path.exists(out) and os.path.exists(stamp):
+        t = os.path.getmtime(out)
+        with open(stamp) as f:
+            same_cmd = f.read() == cmd_text
+        if same_cmd and all(os.path.getmtime(s) <= t for s in sources):
+            return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{r.stdout}\n{r.stderr}")
     os.replace(out + ".tmp", out)
+    with open(stamp, "w") as f:
+        f.write(cmd_text)
     if verbose:
         print(f"built {out}")
     return out

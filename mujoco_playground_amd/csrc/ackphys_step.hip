@@ -383,31 +383,43 @@ struct RayFrame {
 __device__ __forceinline__ RayFrame ray_frame(const float p[3], const float R[9]) {
   return RayFrame{p[0] + R[2] * RAY_Z, p[1] + R[5] * RAY_Z, p[2] + R[8] * RAY_Z, R[0], R[1], R[3], R[4], R[6], R[7]};
 }
-// The same test from the site's chassis-frame origin (ox, oy, RAY_Z) with the full transforms: the
-// lane kernels' observation wave keeps this form (measured: the ring form below made the nc kernel
-// 8.72 -> 8.90 us although it removes ~700 instructions; the quad kernels gain 68.6 -> 68.1 us).
-__device__ __forceinline__ float ray_floor_c(const float p[3], const float R[9], float ox, float oy, float dxb,
-                                             float dyb) {
-  const float dz = R[6] * dxb + R[7] * dyb;
-  const float oz = p[2] + R[6] * ox + R[7] * oy + R[8] * RAY_Z;
-  const float t = -oz * __builtin_amdgcn_rcpf(dz);
-  const float hx = p[0] + R[0] * ox + R[1] * oy + R[2] * RAY_Z + t * (R[0] * dxb + R[1] * dyb);
-  const float hy = p[1] + R[3] * ox + R[4] * oy + R[5] * RAY_Z + t * (R[3] * dxb + R[4] * dyb);
-  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
-  return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
-}
 // chassis-frame direction (dxb, dyb, 0) -> mj_ray's plane test against the finite floor rectangle;
-// distance from the site (t), clamped to the cutoff, -1 for no hit
+// distance from the site (t), clamped to the cutoff, -1 for no hit. The site sits RAY_R out along
+// the ray from the ring centre C, so the plane is met sd = -C_z / d_z from C and t = sd - RAY_R
+// from the site. The hit test combines its terms with a non-short-circuit &: with && the compiler
+// sank the hit-point arithmetic under a per-ray branch (32 s_cbranch per 32 rays, ~27 VALU per ray
+// when the rays can hit); this form is branch-free at ~16 VALU per ray (tools: a 32-ray kernel
+// compiled both ways, 1009 -> 639 VALU).
 __device__ __forceinline__ float ray_floor_f(const RayFrame& F, float dxb, float dyb) {
   const float dz = F.r6 * dxb + F.r7 * dyb;
   const float ux = F.r0 * dxb + F.r1 * dyb, uy = F.r3 * dxb + F.r4 * dyb;
-  const float oz = fmaf(RAY_R, dz, F.c0);
-  // branchless: t from the hardware reciprocal (1 ulp; within the f32 tolerance of the obs parity)
-  const float t = -oz * __builtin_amdgcn_rcpf(dz);
-  const float s = t + RAY_R;
-  const float hx = fmaf(s, ux, F.cx), hy = fmaf(s, uy, F.cy);
-  const bool hit = dz <= -MINVAL && t >= 0.0f && fabsf(hx) <= FLOOR_SIZE[0] && fabsf(hy) <= FLOOR_SIZE[1];
+  const float sd = -F.c0 * __builtin_amdgcn_rcpf(dz);  // hardware reciprocal: 1 ulp, within the obs parity
+  const float hx = fmaf(sd, ux, F.cx), hy = fmaf(sd, uy, F.cy);
+  const float t = sd - RAY_R;
+  bool inside;
+  if constexpr (FLOOR_SIZE[0] == FLOOR_SIZE[1]) inside = fmaxf(fabsf(hx), fabsf(hy)) <= FLOOR_SIZE[0];
+  else inside = (fabsf(hx) <= FLOOR_SIZE[0]) & (fabsf(hy) <= FLOOR_SIZE[1]);
+  const bool hit = (dz <= -MINVAL) & (t >= 0.0f) & inside;
   return hit ? fminf(t, RAY_CUTOFF) : -1.0f;
+}
+// The ring's bounding test (mj_ray culls geoms by their extent before the exact test; this culls
+// the 72 floor tests at once, and is exact: it only reports "every ray misses" when every ray's own
+// test above returns -1). All rays lie in the chassis plane z = RAY_Z, so a ray's world direction d
+// has |d_z| <= A = |(R20, R21)| and |d_xy| >= sqrt(1 - A^2). Ring below the floor (centre height
+// C_z < 0): a downward ray starts at C_z + RAY_R d_z < 0 and meets the plane behind it (t < 0); an
+// upward one fails d_z <= -MINVAL. Ring above: a downward ray meets the plane at s = C_z / |d_z| >=
+// C_z / A from the centre, horizontally s |d_xy| from the centre's foot point, which must be within
+// |C_xy| + |FLOOR_SIZE| for a hit on the floor rectangle. The margins (1e-4 relative below, 0.2 %
+// and 1 m above) dwarf the f32 rounding of the per-ray tests; the transition band is cast in full.
+// Why it matters: on the flat floor most readings are -1 (a level robot's rays never reach the
+// floor within its 40 m extent), and casting 62 rays is ~2.3k of the observation waves' cycles.
+__device__ __forceinline__ bool floor_rays_all_miss(const float p[3], const float R[9]) {
+  const float cz = p[2] + R[8] * RAY_Z;
+  if (cz < -1e-4f * (1.0f + fabsf(p[2]))) return true;
+  const float a2 = R[6] * R[6] + R[7] * R[7];
+  const float reach = fabsf(p[0] + R[2] * RAY_Z) + fabsf(p[1] + R[5] * RAY_Z) +
+                      sqrtf(FLOOR_SIZE[0] * FLOOR_SIZE[0] + FLOOR_SIZE[1] * FLOOR_SIZE[1]) + 1.0f;
+  return cz > 0.0f && cz * cz * (1.0f - a2) > 1.002f * a2 * reach * reach;
 }
 
 // ------------------------------------------------------------------ impedance / reference
@@ -462,14 +474,20 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   // ackermann_env.py:131-141); the min over the 72 aliased readings is the min over rays 10..71.
   float minl = 3.0e38f, v71 = -1.0f;
   const RayFrame F = ray_frame(p, R);
+  if (SC == 0 && __builtin_amdgcn_ballot_w64(!floor_rays_all_miss(p, R)) == 0ull) {
 #pragma unroll
-  for (int i = RFIRST; i < 72; i++) {
-    float v;
-    if constexpr (SC == 0) v = ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
-    else v = ray_scene<SC>(F, RAY_DIR[i][0], RAY_DIR[i][1]);
-    stf(dst, i, vo, v);
-    minl = fminf(minl, v);
-    v71 = v;
+    for (int i = RFIRST; i < 72; i++) stf(dst, i, vo, -1.0f);
+    minl = -1.0f;
+  } else {
+#pragma unroll
+    for (int i = RFIRST; i < 72; i++) {
+      float v;
+      if constexpr (SC == 0) v = ray_floor_f(F, RAY_DIR[i][0], RAY_DIR[i][1]);
+      else v = ray_scene<SC>(F, RAY_DIR[i][0], RAY_DIR[i][1]);
+      stf(dst, i, vo, v);
+      minl = fminf(minl, v);
+      v71 = v;
+    }
   }
   STAMP(12);
 #pragma unroll
@@ -1657,6 +1675,9 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
   // steer pairs the equality does not hold together); a miss continues with Newton from the
   // piece's minimiser, which is a start as good as any.
   bool exact = false;
+#ifdef AK_STAMPS
+  int diag_pair = 0;  // diag build: 1 = this lane's one-dof steer guess was inconsistent (9-pair search)
+#endif
   if constexpr (NC && AK_NC_PREDICT) {
     float ap[NV];
 #pragma unroll
@@ -1699,6 +1720,9 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
         return t1 == s1 && t2 == s2;
       };
       bool ok = consistent(pst[r1], pst[r2]);
+#ifdef AK_STAMPS
+      diag_pair = ok ? 0 : 1;
+#endif
       if (__builtin_amdgcn_ballot_w64(!ok) != 0ull) {
 #pragma unroll 1
         for (int k = 0; k < 9; k++) {
@@ -1926,7 +1950,8 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
   STAMP(6);
   NT_FLUSH;
 #ifdef AK_STAMPS
-  g_stamps[AK_NSTAMP * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] = (unsigned long long)(it_done * 8 + why);
+  g_stamps[AK_NSTAMP * (size_t)gridDim.x + blockIdx.x * 64 + (threadIdx.x & 63)] =
+      (unsigned long long)(it_done * 8 + why) + ((unsigned long long)diag_pair << 16) + ((unsigned long long)!exact << 17);
 #else
   (void)it_done;
   (void)why;
@@ -2605,11 +2630,18 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
       float R[9];
       quat_R(q, R);
       const Soa obs = soa(A.obs, NOBS, n);
+      const RayFrame F = ray_frame(p, R);
+      if (__builtin_amdgcn_ballot_w64(!floor_rays_all_miss(p, R)) == 0ull) {
 #pragma unroll
-      for (int i = 10; i < AK_PREP_RAYS; i++) {
-        const float v = ray_floor_c(p, R, RAY_ORG[i][0], RAY_ORG[i][1], RAY_DIR[i][0], RAY_DIR[i][1]);
-        stf(obs, i, vo, v);
-        mn = fminf(mn, v);
+        for (int i = 10; i < AK_PREP_RAYS; i++) stf(obs, i, vo, -1.0f);
+        mn = -1.0f;
+      } else {
+#pragma unroll
+        for (int i = 10; i < AK_PREP_RAYS; i++) {
+          const float v = ray_floor_f(F, RAY_DIR[i][0], RAY_DIR[i][1]);
+          stf(obs, i, vo, v);
+          mn = fminf(mn, v);
+        }
       }
     }
     xch[XCH_WORDS * 64 + lane] = mn;

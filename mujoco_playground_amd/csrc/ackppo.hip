@@ -7,8 +7,9 @@
 //  * ackppo_act: 16 envs per 256-lane workgroup; weights staged in LDS (W1 transposed, both
 //    layers XOR-swizzled), both layers as 16x16 f32 MFMA tiles (v_mfma_f32_16x16x4_f32; wave w
 //    owns unit tiles 2w, 2w+1 of the 128 actor|critic units), heads + sampling on wave 0.
-//  * ackppo_value / ackppo_bootstrap: lane = env, 64 envs x 16 waves, the waves split the
-//    hidden units (VALU, LDS-broadcast weights).
+//  * ackppo_value / ackppo_bootstrap: the same kernel without the sampling (value only) or
+//    without the policy step (bootstrap only), so every value of a rollout -- per step, the
+//    TimeLimit bootstrap and the last values -- comes from one arithmetic path.
 //  * ackppo_grad: one 256-lane workgroup per 32-sample tile. Forward layers, the W2^T backward
 //    and the weight-gradient sums over the tile (kept in the MFMA accumulators across tiles)
 //    are f32 MFMA tiles; heads, loss gradient and d2 on the VALU; every activation / delta
@@ -88,66 +89,6 @@ __device__ __forceinline__ float gauss_term(float a, float mu, float ls) {
   const float dv = a - mu;
   return -0.5f * dv * dv * fexp(-2.0f * ls) - ls - LOG_SQRT_2PI;
 }
-// out[j] = tanh(b[j] + W[j,:] . x) for the 64 units, written to an LDS column (stride cs).
-// W/b addresses are wave-uniform: scalar loads, x stays in VGPRs.
-template <int IN>
-__device__ __forceinline__ void dense_tanh(const float* __restrict__ W, const float* __restrict__ b,
-                                           const float (&x)[IN], float* col, int cs) {
-_Pragma(PP_UNROLL_STR)
-  for (int j = 0; j < H; j++) {
-    float acc = 0.0f;
-#pragma unroll
-    for (int k = 0; k < IN; k++) acc = fmaf(W[j * IN + k], x[k], acc);
-    col[j * cs] = ftanh(acc + b[j]);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void load_col(const float* col, int cs, float (&h)[N]) {
-#pragma unroll
-  for (int k = 0; k < N; k++) h[k] = col[k * cs];
-}
-
-// trunk of one net: x -> h2 (registers); h1 and h2 also left in LDS columns c1 / c2
-__device__ __forceinline__ void trunk(const float* __restrict__ p, const Net net, const float (&x)[NOBS], float* c1,
-                                      float* c2, int cs, float (&h)[H]) {
-  dense_tanh<NOBS>(p + net.w1, p + net.b1, x, c1, cs);
-  load_col(c1, cs, h);
-  dense_tanh<H>(p + net.w2, p + net.b2, h, c2, cs);
-  load_col(c2, cs, h);
-}
-
-__device__ __forceinline__ float critic_head(const float* __restrict__ p, const float (&h)[H]) {
-  float v = 0.0f;
-#pragma unroll
-  for (int j = 0; j < H; j++) v = fmaf(p[ACKPPO_OFF_VAL_W + j], h[j], v);
-  return v + p[ACKPPO_OFF_VAL_B];
-}
-
-__device__ __forceinline__ void actor_head(const float* __restrict__ p, const float (&h)[H], float mu[NA]) {
-#pragma unroll
-  for (int d = 0; d < NA; d++) {
-    float m = 0.0f;
-#pragma unroll
-    for (int j = 0; j < H; j++) m = fmaf(p[ACKPPO_OFF_ACT_W + d * H + j], h[j], m);
-    mu[d] = m + p[ACKPPO_OFF_ACT_B + d];
-  }
-}
-
-// torch.distributions.Normal.log_prob summed over the action dims (SB3 DiagGaussianDistribution)
-__device__ __forceinline__ float gauss_logp(const float a[NA], const float mu[NA], const float* __restrict__ p) {
-  float lp = 0.0f;
-#pragma unroll
-  for (int d = 0; d < NA; d++) {
-    lp += gauss_term(a[d], mu[d], p[ACKPPO_OFF_LOG_STD + d]);
-  }
-  return lp;
-}
-
-__device__ __forceinline__ void load_obs_soa(const float* obs, int n, int e, float (&x)[NOBS]) {
-#pragma unroll
-  for (int k = 0; k < NOBS; k++) x[k] = obs[(size_t)k * n + e];
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -184,130 +125,6 @@ struct ActArgs {
   float* done_out;
 };
 
-// Policy tile: 64 envs (lane = env) x PT_WAVES waves. The whole parameter vector is staged in
-// LDS once per workgroup (wide coalesced loads) and read back with wave-uniform addresses (LDS
-// broadcast). Waves split the hidden units: wave w computes PT_UPW units of the concatenated
-// actor|critic layers (the first half of the waves the actor, the second the critic),
-// activations exchanged through LDS tiles H1/H2 [128 units][64 envs]. 4096 envs make only 64
-// workgroups, so the latency of a wave's unit loop is the kernel time: 16 waves (4 per SIMD)
-// hide the LDS reads and split the chain 4x finer than one wave per SIMD did (42 us -> see DESIGN).
-#ifndef PT_WAVES
-#define PT_WAVES 16
-#endif
-constexpr int PT_ENVS = 64, PT_THREADS = 64 * PT_WAVES, PT_HALF = PT_WAVES / 2, PT_UPW = H / PT_HALF;
-static_assert(H % PT_HALF == 0 && PT_WAVES >= 4, "policy tile split");
-struct PolicyLds {
-  float w[P];
-  float h1[2 * H * PT_ENVS];
-  float h2[2 * H * PT_ENVS];
-};
-
-__device__ __forceinline__ void stage_params(const float* __restrict__ p, float* w) {
-  const float4* src = reinterpret_cast<const float4*>(p);
-  float4* dst = reinterpret_cast<float4*>(w);
-#pragma unroll 4
-  for (int i = threadIdx.x; i < P / 4; i += PT_THREADS) dst[i] = src[i];
-}
-
-// trunks of both nets for the tile; leaves H2 in LDS (caller syncs after)
-__device__ __forceinline__ void policy_trunks(PolicyLds& L, const float (&x)[NOBS], int lane, int wave,
-                                              bool actor, bool critic) {
-  const bool mine = (wave < PT_HALF) ? actor : critic;
-  const Net net = (wave < PT_HALF) ? ACTOR : CRITIC;
-  const int u0 = (wave % PT_HALF) * PT_UPW;   // first unit of this wave within its net
-  const int hrow = (wave / PT_HALF) * H;        // actor rows 0..63, critic rows 64..127
-  if (mine) {
-    const float* W1 = L.w + net.w1;
-    const float* b1 = L.w + net.b1;
-_Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + PT_UPW; u++) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int k = 0; k < NOBS; k++) acc = fmaf(W1[u * NOBS + k], x[k], acc);
-      L.h1[(hrow + u) * PT_ENVS + lane] = ftanh(acc + b1[u]);
-    }
-  }
-  __syncthreads();
-  if (mine) {
-    float h[H];
-#pragma unroll
-    for (int k = 0; k < H; k++) h[k] = L.h1[(hrow + k) * PT_ENVS + lane];
-    const float* W2 = L.w + net.w2;
-    const float* b2 = L.w + net.b2;
-_Pragma(PP_UNROLL_STR)
-    for (int u = u0; u < u0 + PT_UPW; u++) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int k = 0; k < H; k++) acc = fmaf(W2[u * H + k], h[k], acc);
-      L.h2[(hrow + u) * PT_ENVS + lane] = ftanh(acc + b2[u]);
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ float tile_value(const PolicyLds& L, int lane) {
-  float v = 0.0f;
-#pragma unroll 8
-  for (int j = 0; j < H; j++) v = fmaf(L.w[ACKPPO_OFF_VAL_W + j], L.h2[(H + j) * PT_ENVS + lane], v);
-  return v + L.w[ACKPPO_OFF_VAL_B];
-}
-
-__device__ __forceinline__ void tile_mu(const PolicyLds& L, int lane, float mu[NA]) {
-#pragma unroll
-  for (int d = 0; d < NA; d++) {
-    float m = 0.0f;
-#pragma unroll 8
-    for (int j = 0; j < H; j++) m = fmaf(L.w[ACKPPO_OFF_ACT_W + d * H + j], L.h2[j * PT_ENVS + lane], m);
-    mu[d] = m + L.w[ACKPPO_OFF_ACT_B + d];
-  }
-}
-
-extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_value_kernel(const float* params, const float* obs,
-                                                                             int n, float* value) {
-  extern __shared__ float lds_raw[];
-  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int e = blockIdx.x * PT_ENVS + lane;
-  const int ec = e < n ? e : n - 1;
-  stage_params(params, L.w);
-  float x[NOBS];
-  load_obs_soa(obs, n, ec, x);
-  __syncthreads();
-  policy_trunks(L, x, lane, wave, false, true);
-  if (e < n && wave == PT_HALF) value[e] = tile_value(L, lane);
-}
-
-// bootstrap: only tiles holding a truncated (not terminated) env run the critic
-extern "C" __global__ void __launch_bounds__(PT_THREADS) ackppo_bootstrap_kernel(const float* params, const float* tobs,
-                                                                                 const float* reward,
-                                                                                 const uint8_t* term,
-                                                                                 const uint8_t* trunc, int n,
-                                                                                 float gamma, float* reward_out,
-                                                                                 float* done_out) {
-  extern __shared__ float lds_raw[];
-  PolicyLds& L = *reinterpret_cast<PolicyLds*>(lds_raw);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int e = blockIdx.x * PT_ENVS + lane;
-  const bool valid = e < n;
-  const int ec = valid ? e : n - 1;
-  const bool te = term[ec] != 0, tr = trunc[ec] != 0;
-  const bool boot = valid && tr && !te;  // TimeLimit.truncated = truncated and not terminated
-  if (__syncthreads_or(boot)) {
-    stage_params(params, L.w);
-    float x[NOBS];
-    load_obs_soa(tobs, n, ec, x);
-    __syncthreads();
-    policy_trunks(L, x, lane, wave, false, true);
-  }
-  if (valid && wave == PT_HALF) {
-    float r = reward[e];
-    if (boot) r += gamma * tile_value(L, lane);
-    reward_out[e] = r;
-    done_out[e] = (te || tr) ? 1.0f : 0.0f;
-  }
-}
 
 extern "C" __global__ void __launch_bounds__(256) ackppo_gae_kernel(const float* rew, const float* val,
                                                                     const float* starts, const float* last_val,
@@ -1024,6 +841,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
       A.done_out[eb] = (te || tr) ? 1.0f : 0.0f;
     }
   }
+  if (!A.obs) return;  // ackppo_bootstrap: the bootstrap alone (the same critic path as ackppo_act_boot)
   act_load_x(tl, A.obs, A.n, e0, nv, tid);
   __syncthreads();
   if (A.obs_rows) {  // rollout-buffer rows [env][79]: one contiguous block of nv * 79 words
@@ -1037,6 +855,10 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
   const float mu1 = __shfl(v, li + 16, 64), val = __shfl(v, li + 32, 64);
   if (lk != 0 || li >= nv) return;
   const int e = e0 + li;
+  if (!A.env_action) {  // ackppo_value: the critic alone (the same path as the rollout's values)
+    A.value[e] = val;
+    return;
+  }
   const float mu[NA] = {v, mu1};
   float a[NA];
   if (A.deterministic) {
@@ -1263,10 +1085,6 @@ bool policy_lds_ready() {
   const int dev = current_device();
   if (dev < 0) return false;
   if (g_policy_attr[dev]) return true;
-  const void* ks[2] = {(const void*)ackppo_value_kernel, (const void*)ackppo_bootstrap_kernel};
-  for (const void* k : ks)
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(PolicyLds)) != hipSuccess)
-      return false;
   if (hipFuncSetAttribute((const void*)ackppo_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACT_LDS) !=
       hipSuccess)
     return false;
@@ -1318,8 +1136,11 @@ int ackppo_value(const float* params, const float* obs_soa, int n_env, float* va
   if (!params || !obs_soa || !value || n_env < 0) return fail(ACKPPO_EINVAL, "ackppo_value: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
   if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_value: cannot reserve the policy LDS tile");
-  hipLaunchKernelGGL(ackppo_value_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS), sizeof(PolicyLds),
-                     (hipStream_t)stream, params, obs_soa, n_env, value);
+  // the act kernel without sampling: the same critic arithmetic as the rollout's per-step values
+  ActArgs A{params,  obs_soa, n_env,   0,       0,       0,       1,      nullptr, nullptr, nullptr,
+            nullptr, value,   nullptr, nullptr, nullptr, nullptr, 0.0f, nullptr, nullptr};
+  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + AE - 1) / AE), dim3(GRAD_THREADS), ACT_LDS, (hipStream_t)stream,
+                     A);
   return launched("ackppo_value");
 }
 
@@ -1329,9 +1150,11 @@ int ackppo_bootstrap(const float* params, const float* terminal_obs_soa, const f
     return fail(ACKPPO_EINVAL, "ackppo_bootstrap: bad arguments");
   if (n_env == 0) return ACKPPO_OK;
   if (!policy_lds_ready()) return fail(ACKPPO_EHIP, "ackppo_bootstrap: cannot reserve the policy LDS tile");
-  hipLaunchKernelGGL(ackppo_bootstrap_kernel, dim3((n_env + PT_ENVS - 1) / PT_ENVS), dim3(PT_THREADS),
-                     sizeof(PolicyLds), (hipStream_t)stream, params, terminal_obs_soa, reward, term, trunc, n_env,
-                     gamma, reward_out, done_out);
+  // the act kernel's bootstrap part alone (obs == nullptr): bit-identical to ackppo_act_boot's
+  ActArgs A{params,  nullptr,          n_env,  0,    0,     0,     1,          nullptr, nullptr, nullptr,
+            nullptr, nullptr, terminal_obs_soa, reward, term, trunc, gamma, reward_out, done_out};
+  hipLaunchKernelGGL(ackppo_act_kernel, dim3((n_env + AE - 1) / AE), dim3(GRAD_THREADS), ACT_LDS, (hipStream_t)stream,
+                     A);
   return launched("ackppo_bootstrap");
 }
 

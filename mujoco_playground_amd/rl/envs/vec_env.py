@@ -8,6 +8,8 @@ Tensors stay on the GPU; obs is a [N,79] view of the kernel's [79,N] SoA buffer.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 from ...sim import BatchedAckermannSim
@@ -21,6 +23,13 @@ class AckermannVecEnv:
                  max_angular_velocity: float = 1.0, render_mode=None, variant: str = "auto",
                  scene: str = "flat"):
         self.num_envs = int(num_envs)
+        # the per-env constructor kwargs of the reference env (ackermann_env.py:51-60), batch-wide here
+        self.max_episode_steps = max_episode_steps
+        self.goal_distance_threshold = goal_distance_threshold
+        self.collision_threshold = collision_threshold
+        self.max_linear_velocity = max_linear_velocity
+        self.max_angular_velocity = max_angular_velocity
+        self.render_mode = render_mode
         self.observation_space = spaces.observation_space()
         self.action_space = spaces.action_space()
         self.sim = BatchedAckermannSim(num_envs, device, seed=seed, contacts=contacts, env_offset=env_offset,
@@ -34,6 +43,7 @@ class AckermannVecEnv:
         self._actions = None
         self._ep_ret = torch.zeros(self.num_envs, device=self.device)
         self._ep_len = torch.zeros(self.num_envs, device=self.device)
+        self._t_start = time.time()
 
     # -------- SB3 VecEnv API
     def reset(self) -> torch.Tensor:
@@ -74,7 +84,9 @@ class AckermannVecEnv:
             for j, i in enumerate(idx):
                 out[i]["terminal_observation"] = tobs[j]
                 out[i]["TimeLimit.truncated"] = bool(tr[j]) and not bool(tm[j])
-                out[i]["episode"] = {"r": rets[j], "l": int(lens[j])}
+                # Monitor's episode record: return, length, wall time since the env was made (train.py:70)
+                out[i]["episode"] = {"r": round(rets[j], 6), "l": int(lens[j]),
+                                     "t": round(time.time() - self._t_start, 6)}
         return out
 
     def env_info(self) -> dict:

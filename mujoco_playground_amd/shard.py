@@ -27,6 +27,8 @@ def init(backend: str | None = None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or os.environ.get("ACKPHYS_DIST_BACKEND") or (
             "nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":  # RCCL binds the rank's communicator to its current device
+            torch.cuda.set_device(device_for(local))
         dist.init_process_group(backend=backend)
     return rank, world, local
 

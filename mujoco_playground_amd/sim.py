@@ -153,7 +153,49 @@ class BatchedAckermannSim:
             _lib.check(rc, "ackphys_rollout")
         if per_step_outputs:
             self.last_rollout = {"terminal_obs": tobs, "info": info}
+            # the single-step buffers hold step K-1's outputs afterwards, as after K `step` calls
+            # (a policy or the VecEnv reading sim.obs_soa next must see the current observation)
+            self.obs_soa.copy_(obs[-1])
+            self.reward.copy_(rew[-1])
+            self.term.copy_(term[-1])
+            self.trunc.copy_(trunc[-1])
+            if info is not None:
+                self.info.copy_(info[-1])
+            if tobs is not None:  # written only for envs done at step K-1 (earlier rows stay as step wrote them)
+                done = (term[-1] | trunc[-1]).bool()
+                if k > 1:  # an env done at an earlier step keeps that step's terminal row, as in K step calls
+                    done_any = (term[:-1] | trunc[:-1]).bool()
+                    last = torch.where(done_any, torch.arange(k - 1, device=self.device)[:, None], -1).amax(0)
+                    earlier = (last >= 0) & ~done
+                    rows = tobs.gather(0, last.clamp(min=0)[None, None, :].expand(1, NOBS, self.n))[0]
+                    self.terminal_obs_soa.copy_(torch.where(earlier[None, :], rows, self.terminal_obs_soa))
+                self.terminal_obs_soa.copy_(torch.where(done[None, :], tobs[-1], self.terminal_obs_soa))
         return obs, rew, term, trunc
+
+    def rollout_launcher(self, actions: torch.Tensor, autoreset: bool = True, want_info: bool = False,
+                         want_terminal: bool = False, track_episodes: bool = True):
+        """A zero-argument callable that launches `rollout(actions, per_step_outputs=False)` on the
+        current stream: every C argument is converted once, here, so a launch costs one ctypes call
+        (for timed windows of a few tens of microseconds, where the Python checks and argument
+        conversion of `rollout` are a visible share of the host clock)."""
+        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+            raise ValueError("rollout_launcher: actions must be a contiguous float32 tensor on the sim's device")
+        if actions.dim() != 3 or actions.shape[1:] != (self.n, 2) or actions.shape[0] < 1:
+            raise ValueError(f"actions must be [K, {self.n}, 2], got {tuple(actions.shape)}")
+        fn = _lib.lib().ackphys_rollout
+        c = self._c
+        flags = self.flags | (AUTORESET if autoreset else 0)
+        args = (self._ctx, C.c_int(int(actions.shape[0])), C.c_void_p(actions.data_ptr()), c["state"], c["obs_soa"],
+                c["reward"], c["term"], c["trunc"], c["terminal_obs_soa"] if (autoreset and want_terminal) else None,
+                c["info"] if want_info else None, c["episode"] if track_episodes else None, C.c_uint32(flags),
+                C.c_uint64(self.seed), C.c_int(0), C.c_void_p(_raw_stream(self._dev_index)))
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _lib.check(rc, "ackphys_rollout")
+        launch.actions = actions  # keeps the action buffer alive as long as the launcher
+        return launch
 
     def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:
         """[K, N, 2] i.i.d. U[-1,1) actions from Philox(seed; env, step) on device."""

@@ -100,6 +100,15 @@ def test_act_boot_equals_act_plus_bootstrap():
     np.testing.assert_array_equal(do.cpu().numpy(), d_ref)
     boot = (trunc == 1) & (term == 0)
     assert np.array_equal(ro.cpu().numpy()[~boot], rew[~boot]) and not np.allclose(r_ref[boot], rew[boot])
+    # the rollout's last step bootstraps through ackppo_bootstrap: bit for bit the same rewards and
+    # flags as act_boot gives every other step (one critic path for the whole rollout)
+    rb, db = torch.full((n,), -7.0, device=DEV), torch.full((n,), -7.0, device=DEV)
+    assert L().ackppo_bootstrap(P(p), P(tsoa), P(t(rew)), P(t(term)), P(t(trunc)), n, 0.99, P(rb), P(db), S()) == 0
+    vv = torch.zeros(n, device=DEV)
+    assert L().ackppo_value(P(p), P(soa), n, P(vv), S()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(rb, ro) and torch.equal(db, do)
+    assert torch.equal(vv, a1[4])  # ackppo_value = the act kernel's values bit for bit
 
 
 def test_checkpoint_policy_on_gpu():

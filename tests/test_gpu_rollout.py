@@ -75,6 +75,10 @@ def test_rollout_equals_steps(scene, contacts, variant, poststep):
         assert not tobs[k][:, ~done].any(), "terminal obs written for an env that was not done"
     assert torch.equal(a.state, b.state)
     assert torch.equal(a.episode, b.episode)
+    # the single-step buffers hold step K-1's outputs afterwards (a policy reads a.obs_soa next),
+    # and every env's terminal-obs row is the one of its last done step, as after K step calls
+    for name in ("obs_soa", "reward", "term", "trunc", "info", "terminal_obs_soa"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), f"single-step buffer {name} is stale"
     assert dones >= n  # every env truncated at least once inside the launch (eplen 9, 23 steps)
     assert bool(info[0][3, 7]) and bool(info[0][3, 150])  # the poisoned envs were reset (bad_state)
 
@@ -121,6 +125,7 @@ def test_rollout_full_episode_4096(scene, contacts):
     assert torch.equal(rew, rb)
     assert torch.equal(term | (trunc << 1), tb)
     assert torch.equal(obs[-1], b.obs_soa)
+    assert torch.equal(a.obs_soa, b.obs_soa)
     assert torch.equal(a.state, b.state)
     assert torch.equal(a.episode, b.episode)
     assert int(trunc[999].sum()) == n - int(term[:999].any(0).sum())  # envs not terminated earlier

@@ -93,6 +93,67 @@ def test_free_fall_closed_form(oracle):
         assert abs(st[0, 15] + g * h * k) < 1e-12
 
 
+# rear drive (ackermann_robot_v2.xml:119-121: velocity servo kv 1) on a rear wheel joint (:44-51:
+# damping 0.15, frictionloss 0.02); steering servo (:113-117: kp 40, kv 6, forcerange +-2)
+KV_REAR, B_REAR, FLOSS_REAR = 1.0, 0.15, 0.02
+KP_STEER, KV_STEER, FMAX_STEER = 40.0, 6.0, 2.0
+QVEL_RL, QVEL_RR, QVEL_FL_STEER, QPOS_FL_STEER = 6, 7, 8, 9
+
+
+def wheel_steady_state(c):
+    """With contacts off the wheels spin free. At a steady spin (qacc = 0) the rear wheel's
+    generalised forces balance: kv (c - w) = b w + floss sign(w) (the friction-loss row saturates at
+    +-floss once |w| is far above its Huber zone), so w* = (kv c - floss sign c) / (kv + b)."""
+    c = np.asarray(c, dtype=np.float64)
+    return (KV_REAR * c - FLOSS_REAR * np.sign(c)) / (KV_REAR + B_REAR)
+
+
+def steer_servo_force(ctrl, q, qdot):
+    return np.clip(KP_STEER * (ctrl - q) - KV_STEER * qdot, -FMAX_STEER, FMAX_STEER)
+
+
+def test_free_wheel_steady_state_closed_form(oracle):
+    from oracle.oracle import controller
+    acts = np.array([[0.5, 0.0], [0.2, 0.0], [-0.7, 0.0], [1.0, 0.0], [0.5, 0.5], [-0.3, -0.8]], np.float32)
+    st = np.zeros((len(acts), 44))
+    oracle.reset(st, seed=0)
+    for _ in range(300):
+        oracle.step(st, acts, flags=0)
+    ctrl = np.array([controller(a) for a in acts])
+    w = wheel_steady_state(ctrl[:, 1:3])
+    # straight: exact to rounding; turning: the steering servo's limit cycle (below) shakes the
+    # chassis and couples into the wheel joints at the 1e-7 level
+    rtol = np.where(acts[:, 1] == 0, 1e-9, 1e-6)
+    for j, dof in enumerate((QVEL_RL, QVEL_RR)):
+        assert np.all(np.abs(st[:, 13 + dof] - w[:, j]) <= rtol * np.abs(w[:, j])), (st[:, 13 + dof], w[:, j])
+
+
+def test_steering_servo_period_two_limit_cycle(oracle):
+    """SURVEY finding 8: the steer axis inertia is so small that kv dt / I >> 2, and MuJoCo does not
+    integrate the actuator's kv term implicitly, so the servo never settles: once the transient is
+    over its force sits on the force limit with the sign flipping every step and the steer
+    velocity alternates +-v (a period-2 limit cycle) whose amplitude is the same whatever the
+    target (targets away from the +-35 deg joint limits, whose rows would enter the cycle)."""
+    from oracle.oracle import controller
+    acts = np.array([[0.5, 0.5], [0.3, -0.4], [0.6, -0.2], [0.8, 0.1]], np.float32)
+    ctrl = np.array([controller(a) for a in acts])
+    st = np.zeros((len(acts), 44))
+    oracle.reset(st, seed=0)
+    F, v = [], []
+    for k in range(300):
+        F.append(steer_servo_force(ctrl[:, 0], st[:, QPOS_FL_STEER], st[:, 13 + QVEL_FL_STEER]))
+        v.append(st[:, 13 + QVEL_FL_STEER].copy())
+        oracle.step(st, acts, flags=0)
+    F, v = np.array(F[100:]), np.array(v[100:])
+    assert np.all(np.abs(F) == FMAX_STEER)                 # saturated every step
+    assert np.all(F[1:] * F[:-1] < 0)                      # sign alternates every step
+    assert np.all(v[1:] * v[:-1] < 0)
+    amp = np.abs(v)
+    assert np.all(np.abs(amp - amp.mean(0)) < 5e-3 * amp.mean(0))  # constant amplitude (period 2)
+    m = amp.mean(0)
+    assert np.all(np.abs(m - m.mean()) < 1e-4 * m.mean()) and 2.2 < m.mean() < 2.4  # target-independent
+
+
 def test_static_rest_normal_force(oracle):
     st = np.zeros((1, 44))
     oracle.reset(st, seed=0)

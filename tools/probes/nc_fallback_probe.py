@@ -58,7 +58,7 @@ def main():
         L.ackphys_step(ctx4, p(acts4[k]), p(state4), p(obs4), p(rew4), p(term4), p(trunc4), None, None, None, 2, 0,
                        stream)
         torch.cuda.synchronize()
-        it = st4.cpu().numpy()[NSTAMP * nb4: NSTAMP * nb4 + 64 * nb4] // 8
+        it = (st4.cpu().numpy()[NSTAMP * nb4: NSTAMP * nb4 + 64 * nb4] & 0xFF) // 8
         w = it.reshape(-1, 64).max(1)
         print(f"bench step {k}: lane hist {np.bincount(it, minlength=4)[:6]} wave-max hist {np.bincount(w, minlength=4)[:6]}")
     assert L.ackphys_diag_set_stamps(p(stamps)) == 0
@@ -82,7 +82,7 @@ def main():
             L.ackphys_step(ctx, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None, 2, seed,
                            stream)
             torch.cuda.synchronize()
-            it = stamps.cpu().numpy()[NSTAMP * nb: NSTAMP * nb + 64 * nb] // 8
+            it = (stamps.cpu().numpy()[NSTAMP * nb: NSTAMP * nb + 64 * nb] & 0xFF) // 8
             print(f"seed {seed} step {k}: Newton iterations after the predicted piece, lane hist "
                   f"{np.bincount(it, minlength=4)[:8]}")
 

@@ -1,14 +1,17 @@
 """rocprofv3 PMC passes for the step kernels -> gpurun_out/pmc_latest.json (run on the GPU box).
 
 For each workload (contacts off -> ackphys_rollout_nc_kernel, contacts on -> ackphys_rollout_quad_kernel,
-the kernels bench.py's AUTO mapping runs; one launch = the K timed steps) three separate passes,
-kernel-trace only, no sys/runtime trace:
+the kernels bench.py's AUTO mapping runs; one launch = the K timed steps) and each K in KS, three
+separate passes, kernel-trace only, no sys/runtime trace:
   FETCH_SIZE, WRITE_SIZE (HBM bytes; they do not fit one TCC pass on gfx950),
   SQ_INSTS_VALU + SQ_INSTS_SALU + SQ_WAVES (instruction mix, one SQ pass).
 Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 128-B requests at 64 B for
 lane-contiguous streaming reads -> doubled; WRITE_SIZE taken as reported. The counters of the
-timed launch (the kernel's last dispatch) are divided by its K steps: bytes and instructions per step.
-    python3 tools/profile_pmc.py
+timed launch (the kernel's last dispatch) are divided by its K steps: bytes and instructions per
+step. Entries are keyed "<kernel>@K<k>"; bench.py reports the entry whose K equals its --steps (or
+the nearest K, saying so), since a launch's first-step loads and last-step stores are spread over
+its K steps.
+    python3 tools/profile_pmc.py [K,K,...]     (default 20,1000: the driver's and bench's defaults)
 """
 import csv
 import glob
@@ -19,14 +22,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {0: "ackphys_rollout_nc_kernel", 1: "ackphys_rollout_quad_kernel"}
-K = 60  # timed steps = steps of the profiled launch
+KS = [int(k) for k in (sys.argv[1] if len(sys.argv) > 1 else "20,1000").split(",")]
 
 
-def run_pass(counters, out, contacts):
+def run_pass(counters, out, contacts, k):
     os.makedirs(out, exist_ok=True)
-    cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
+    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
            "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
-           "--no-obstacles", "--steps", str(K), "--warmup", "5", "--contacts", str(contacts)]
+           "--no-obstacles", "--no-per-step", "--steps", str(k), "--warmup", "5", "--contacts", str(contacts)]
     env = dict(os.environ, TMPDIR="/tmp")
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, stdout=subprocess.DEVNULL)
     vals = {c: {} for c in counters}  # counter -> dispatch id -> value (summed over the rows of a dispatch)
@@ -41,22 +44,24 @@ def run_pass(counters, out, contacts):
 
 def main():
     res = {}
-    for contacts, kern in KERNELS.items():
-        out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}")
-        f = run_pass(["FETCH_SIZE"], out + "_fetch", contacts)["FETCH_SIZE"]
-        w = run_pass(["WRITE_SIZE"], out + "_write", contacts)["WRITE_SIZE"]
-        sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts)
-        res[kern] = {
-            "contacts": bool(contacts), "launch_steps": K, "FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w,
-            "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if (f is not None and w is not None) else None,
-            "hbm_bytes_per_step": (2 * f * 1024 + w * 1024) / K if (f is not None and w is not None) else None,
-            "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
-            "algorithmic_bytes_per_step": 690 * 4096,
-            "SQ_INSTS_VALU": sq["SQ_INSTS_VALU"], "SQ_INSTS_SALU": sq["SQ_INSTS_SALU"], "SQ_WAVES": sq["SQ_WAVES"],
-            "valu_insts_per_wave_step": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] / K) if sq["SQ_WAVES"] else None,
-        }
+    for k in KS:
+        for contacts, kern in KERNELS.items():
+            out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}_k{k}")
+            f = run_pass(["FETCH_SIZE"], out + "_fetch", contacts, k)["FETCH_SIZE"]
+            w = run_pass(["WRITE_SIZE"], out + "_write", contacts, k)["WRITE_SIZE"]
+            sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts, k)
+            ok = f is not None and w is not None
+            res[f"{kern}@K{k}"] = {
+                "kernel": kern, "contacts": bool(contacts), "launch_steps": k, "FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w,
+                "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if ok else None,
+                "hbm_bytes_per_step": (2 * f * 1024 + w * 1024) / k if ok else None,
+                "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
+                "algorithmic_bytes_per_step": 690 * 4096,
+                "SQ_INSTS_VALU": sq["SQ_INSTS_VALU"], "SQ_INSTS_SALU": sq["SQ_INSTS_SALU"], "SQ_WAVES": sq["SQ_WAVES"],
+                "valu_insts_per_wave_step": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] / k) if sq["SQ_WAVES"] else None,
+            }
+            print(json.dumps({f"{kern}@K{k}": res[f"{kern}@K{k}"]}), flush=True)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest.json"), "w"), indent=1)
-    print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":

@@ -69,6 +69,7 @@ def main():
     stream = P(torch.cuda.current_stream().cuda_stream)
     acts = torch.zeros(300, n, 2, device=dev)
     L.ackphys_random_actions(ctx, p(acts), 300, 0, 0, stream)
+    summary = {}
     for flags, label in [(2, "contacts OFF"), (3, "contacts ON")]:
         state.zero_()
         L.ackphys_reset(ctx, None, 0, p(state), p(obs), stream)
@@ -119,6 +120,18 @@ def main():
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
         for (_, _, name), v in zip(phases, d):
             print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
+        kern = "obst_kernel" if obst else ("quad_kernel" if quad else ("nc_kernel" if flags == 2 else "kernel"))
+        summary[label] = {"kernel": ("ackphys_rollout_" if ROLL > 1 else "ackphys_step_") + kern,
+                          "dyn_wave_cycles_per_step_median": float(tot),
+                          "dyn_wave_cycles_per_step_max": float(np.max(np.concatenate(spans))),
+                          "phases_median": {name: float(v) for (_, _, name), v in zip(phases, d)},
+                          "measured": "diag build (s_memtime stamps, ~+11 % cycles), 4096 envs, steps 200-209 after "
+                                      "reset, " + (f"last step of {ROLL}-step rollout launches" if ROLL > 1
+                                                   else "single-step launches")}
+    if os.environ.get("STAMPS_JSON"):
+        import json
+        with open(os.environ["STAMPS_JSON"], "w") as f:
+            json.dump(summary, f, indent=1)
 
 
 if __name__ == "__main__":
