@@ -86,8 +86,8 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     shard.barrier(world, device)
     torch.cuda.synchronize(device)
     gc.disable()  # no collector pass inside the host-clocked window
+    ev0.record(stream)  # enqueued before the clock starts: the window holds the launch(es) and the drain
     t0 = time.perf_counter()
-    ev0.record(stream)
     if g is not None:
         g.replay()
     elif per_step:
@@ -153,6 +153,8 @@ def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_
             "rollout_env_steps_per_s": n_steps * n_env * world / (roll_ms * 1e-3),
             "rollout_ms": roll_ms, "update_ms": train_ms, "minibatch_updates_per_iter": nmb * n_epochs,
             "update_us_per_minibatch": train_ms * 1e3 / (nmb * n_epochs),
+            "rollout_path": ("one ackphys_ppo_rollout launch per rollout (policy + env steps + bootstrap fused)"
+                             if model.fused_rollout else "ackppo_act + ackphys_step launches per step"),
             "config": f"{scene} scene, {n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} "
                       f"ranks, {n_epochs} epochs, contacts on, {iters} timed iterations after 1 warm-up",
             "last_logger": {k: v for k, v in model.logger.items() if isinstance(v, (int, float)) or v is None}}

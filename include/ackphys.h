@@ -113,6 +113,25 @@ int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* st
  * observation at the reset state. */
 int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* state, float* obs, void* stream);
 
+/* Policy-in-the-loop PPO rollout of n_steps steps in ONE launch (BASELINE configs[3]): exactly the
+ * per-step loop of stable-baselines3's collect_rollouts (src/rl/train.py:175-179) as libackppo runs
+ * it -- ackppo_act (ackppo_act_boot) + ackphys_step with auto-reset + ackppo_bootstrap after the last
+ * step + ackppo_value -- with the same results bit for bit. params: the flat policy vector of
+ * include/ackppo.h; policy_seed / step0: the action noise's Philox key and the step counter of
+ * rollout step 0 (step t uses step0 + t); deterministic != 0: actions = mean.
+ * Sim buffers as for ackphys_step (in place, holding step n_steps-1's outputs afterwards; obs is
+ * read as the observation of step 0 and left as the one after the last step); terminal_obs and
+ * episode nullable. Rollout buffer (T = n_steps, N = n_env): obs_rows [T*N][79], actions [T*N][2]
+ * (unclipped samples), log_prob / value / rollout_reward (with the TimeLimit bootstrap) /
+ * episode_starts [T][N] (row 0 is the caller's: the previous rollout's last_dones), last_dones [N],
+ * last_values [N]. Needs flags ACKPHYS_CONTACTS | ACKPHYS_AUTORESET (no ACKPHYS_POSTSTEP_OBS) and the
+ * quad mapping (variant AUTO or QUAD). Replaces the reference's DummyVecEnv.step loop under SB3. */
+int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32_t step0, uint64_t policy_seed,
+                        int deterministic, float gamma, float* state, float* obs, float* reward, uint8_t* term,
+                        uint8_t* trunc, float* terminal_obs, float* episode, float* obs_rows, float* actions,
+                        float* log_prob, float* value, float* rollout_reward, float* episode_starts, float* last_dones,
+                        float* last_values, uint32_t flags, uint64_t seed, void* stream);
+
 /* Fill actions[K][N][2] with i.i.d. U[-1,1) from Philox4x32-10 keyed by seed, counter
  * (env_offset + env, step0 + k, 1, 0): the benchmark's synthetic "random ctrl" input. */
 int ackphys_random_actions(ackphys_t* ctx, float* actions, int k_steps, uint64_t seed, uint32_t step0, void* stream);

@@ -46,7 +46,8 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 # v_pk_*_f32, which needs operand pairs in consecutive registers: in these register-bound,
 # one-wave-per-SIMD kernels that cost more in moves and AGPR spills than it saved (nc kernel:
 # 10.9k -> 9.4k static instructions, 1109 -> 357 v_mov; measured 14.78 -> 13.67 us per step,
-# contacts-on quad 75.4 -> 70.1 us, obstacles 82.3 -> 76.6 us). The PPO kernels measured even.
+# contacts-on quad 75.4 -> 70.1 us, obstacles 82.3 -> 76.6 us). The PPO kernels measured even, and
+# share it so the policy code common to both libraries compiles alike.
 PHYS_FLAGS = ["-fno-slp-vectorize"]
 
 
@@ -89,12 +90,14 @@ def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = (
 def build(verbose: bool = False, force: bool = False) -> str:
     """Compile the HIP sources for gfx950 into csrc/build/ (in-tree): libackphys.so (physics
     step, include/ackphys.h) and libackppo.so (PPO learner, include/ackppo.h)."""
-    _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force)
+    # both libraries with the same flags: the policy arithmetic they share (csrc/ackppo_math.inc)
+    # then compiles alike, and the fused rollout's actions equal ackppo_act's bit for bit
+    _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force, tuple(PHYS_FLAGS))
     return _hipcc(LIB_PATH, SOURCES, verbose, force, tuple(PHYS_FLAGS))
 
 
 EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackphys_set_variant", "ackphys_set_env_offset", "ackphys_step", "ackphys_rollout",
-           "ackphys_reset",
+           "ackphys_ppo_rollout", "ackphys_reset",
            "ackphys_random_actions", "ackphys_model_fnv", "ackphys_last_error", "ackphys_version"]
 
 PPO_EXPORTS = ["ackppo_act", "ackppo_act_boot", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
@@ -126,6 +129,7 @@ def lib():
     L.ackphys_set_env_params.argtypes = [P, C.POINTER(EnvParams)]
     L.ackphys_step.argtypes = [P, P, P, P, P, P, P, P, P, P, u32, u64, P]
     L.ackphys_rollout.argtypes = [P, i32, P, P, P, P, P, P, P, P, P, u32, u64, i32, P]
+    L.ackphys_ppo_rollout.argtypes = [P, P, i32, u32, u64, i32, C.c_float] + [P] * 15 + [u32, u64, P]
     L.ackphys_reset.argtypes = [P, P, u64, P, P, P]
     L.ackphys_random_actions.argtypes = [P, P, i32, u64, u32, P]
     L.ackphys_model_fnv.restype = u64

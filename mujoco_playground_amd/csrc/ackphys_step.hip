@@ -2081,6 +2081,7 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
 }  // namespace ak
 
 #include "ackphys_quad.inc"
+#include "ackphys_ppo.inc"
 
 // ====================================================================== kernels
 using namespace ak;
@@ -3015,6 +3016,33 @@ int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* sta
                        ctx->n_env, seed, ctx->env_offset, ctx->prm);
   e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_reset_kernel launch");
+  return ACKPHYS_OK;
+}
+
+int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32_t step0, uint64_t policy_seed,
+                        int deterministic, float gamma, float* state, float* obs, float* reward, uint8_t* term,
+                        uint8_t* trunc, float* terminal_obs, float* episode, float* obs_rows, float* actions,
+                        float* log_prob, float* value, float* rollout_reward, float* episode_starts, float* last_dones,
+                        float* last_values, uint32_t flags, uint64_t seed, void* stream) {
+  if (!ctx || !params || !state || !obs || !reward || !term || !trunc || !obs_rows || !actions || !log_prob ||
+      !value || !rollout_reward || !episode_starts || !last_dones || !last_values)
+    return fail(ACKPHYS_EINVAL, "ackphys_ppo_rollout: NULL argument");
+  if (n_steps <= 0) return fail(ACKPHYS_EINVAL, "ackphys_ppo_rollout: n_steps must be positive");
+  if (!(flags & ACKPHYS_CONTACTS) || !(flags & ACKPHYS_AUTORESET) || (flags & ACKPHYS_POSTSTEP_OBS))
+    return fail(ACKPHYS_EINVAL, "ackphys_ppo_rollout: needs ACKPHYS_CONTACTS | ACKPHYS_AUTORESET (no POSTSTEP_OBS)");
+  if (ctx->variant != ACKPHYS_VARIANT_AUTO && ctx->variant != ACKPHYS_VARIANT_QUAD)
+    return fail(ACKPHYS_EINVAL, "ackphys_ppo_rollout: runs on the quad mapping (variant AUTO or QUAD)");
+  DeviceGuard dg(ctx->device);
+  if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
+  ak::Args a{nullptr, state, obs, reward, term, trunc, terminal_obs, nullptr, episode, ctx->prm, ctx->n_env, flags,
+             seed, ctx->env_offset, ak::PPO_PE};
+  ak::PpoArgs P{params, policy_seed, step0, deterministic, gamma, n_steps, obs_rows, actions, log_prob, value,
+                rollout_reward, episode_starts, last_dones, last_values};
+  const int blocks = (ctx->n_env + ak::PPO_PE - 1) / ak::PPO_PE;
+  hipLaunchKernelGGL(ctx->scene == 1 ? ackphys_ppo_rollout_obst8_kernel : ackphys_ppo_rollout_quad_kernel,
+                     dim3(blocks), dim3(128), 0, (hipStream_t)stream, a, P);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hipfail(e, "ackphys_ppo_rollout launch");
   return ACKPHYS_OK;
 }
 

@@ -23,6 +23,7 @@
 #include <stdio.h>
 
 #include "../../include/ackppo.h"
+#include "ackppo_math.inc"
 
 #ifndef PP_UNROLL
 #define PP_UNROLL 2
@@ -48,47 +49,15 @@ __device__ unsigned long long* g_pp_stamps;
 namespace pp {
 
 constexpr int NOBS = ACKPPO_NOBS, NA = ACKPPO_NACT, H = ACKPPO_HIDDEN, P = ACKPPO_NPARAM;
-constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;
-constexpr float TWO_PI = 6.28318530717958647692f;
-
 struct Net {
   int w1, b1, w2, b2;
 };
 constexpr Net ACTOR{ACKPPO_OFF_PI_W1, ACKPPO_OFF_PI_B1, ACKPPO_OFF_PI_W2, ACKPPO_OFF_PI_B2};
 constexpr Net CRITIC{ACKPPO_OFF_VF_W1, ACKPPO_OFF_VF_B1, ACKPPO_OFF_VF_W2, ACKPPO_OFF_VF_B2};
 
-__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; r++) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
-    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-}
-
-// tanh of the policy's hidden units: Cephes tanhf's form -- |x| < 0.625: x + x^3 P(x^2), else
-// 1 - 2 / (exp(2|x|) + 1) -- with the hardware exp2 / rcp instead of the library's expf and
-// division (a few ulp; the device tanhf is ~2x the instructions). Used by every policy kernel,
-// so the rollout's log_probs and the update's agree exactly.
-__device__ __forceinline__ float ftanh(float x) {
-  const float ax = fabsf(x), z = x * x;
-  const float p = fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z, -5.37397155531e-2f), z,
-                            1.33314422036e-1f), z, -3.33332819422e-1f);
-  const float small = fmaf(x * z, p, x);
-  const float e = __builtin_amdgcn_exp2f(2.88539008178f * ax);  // exp(2|x|); +inf for large |x|
-  const float big = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
-  return ax < 0.625f ? small : big;
-}
-// exp through the hardware exp2 (1 ulp, plus the rounding of x log2 e) and one dimension of the
-// DiagGaussian log-density with std exp(ls): -(a - mu)^2 / (2 exp(2 ls)) - ls - log sqrt(2 pi)
-// (log(exp(ls)) = ls, no division)
-__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504089f); }
-__device__ __forceinline__ float gauss_term(float a, float mu, float ls) {
-  const float dv = a - mu;
-  return -0.5f * dv * dv * fexp(-2.0f * ls) - ls - LOG_SQRT_2PI;
-}
+using ppm::fexp;
+using ppm::ftanh;
+using ppm::gauss_term;
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -388,10 +357,8 @@ constexpr int PERV = (NVEC + GRAD_THREADS - 1) / GRAD_THREADS;
 
 // f32 MFMA 16x16x4 (exact f32 products, k-ordered fmaf chain): lane l supplies A[l & 15][l >> 4]
 // and B[l >> 4][l & 15]; D[row 4 (l >> 4) + r][col l & 15] comes back in element r.
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
+using ppm::f4v;
+using ppm::mfma4;
 
 __device__ __forceinline__ float vec_item(const float* tl, int i) {
   const float* an = tl + G_NET;
@@ -836,7 +803,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
     }
     if (mine) {
       float r = A.reward[eb];
-      if (boot) r += A.gamma * vb;
+      if (boot) r = fmaf(A.gamma, vb, r);
       A.reward_out[eb] = r;
       A.done_out[eb] = (te || tr) ? 1.0f : 0.0f;
     }
@@ -861,33 +828,15 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_act_kernel(Act
   }
   const float mu[NA] = {v, mu1};
   float a[NA];
-  if (A.deterministic) {
-    a[0] = mu[0];
-    a[1] = mu[1];
-  } else {
-    uint32_t c[4] = {(uint32_t)(A.env_offset + e), A.step, 2u, 0u};
-    philox(c, (uint32_t)A.seed, (uint32_t)(A.seed >> 32));
-    const float u1 = (float)((c[0] >> 8) + 1u) * (1.0f / 16777216.0f);  // (0, 1]
-    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);         // [0, 1)
-    const float r = sqrtf(-2.0f * logf(u1));
-    const float z[NA] = {r * cosf(TWO_PI * u2), r * sinf(TWO_PI * u2)};
-#pragma unroll
-    for (int d = 0; d < NA; d++) a[d] = mu[d] + fexp(w[W_LS + d]) * z[d];
-  }
+  const float lp = ppm::sample_action(mu, w[W_LS], w[W_LS + 1], A.deterministic != 0, A.env_offset + e, A.step, A.seed,
+                                      a);
   if (A.action) {
     A.action[2 * (size_t)e] = a[0];
     A.action[2 * (size_t)e + 1] = a[1];
   }
   A.env_action[2 * (size_t)e] = fminf(fmaxf(a[0], -1.0f), 1.0f);
   A.env_action[2 * (size_t)e + 1] = fminf(fmaxf(a[1], -1.0f), 1.0f);
-  if (A.log_prob) {
-    float lp = 0.0f;
-#pragma unroll
-    for (int d = 0; d < NA; d++) {  // gauss_logp with the staged log_std
-      lp += gauss_term(a[d], mu[d], w[W_LS + d]);
-    }
-    A.log_prob[e] = lp;
-  }
+  if (A.log_prob) A.log_prob[e] = lp;
   if (A.value) A.value[e] = val;
 }
 

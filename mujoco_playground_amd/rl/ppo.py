@@ -104,7 +104,8 @@ class PPO:
                  n_epochs: int = 10, gamma: float = 0.99, gae_lambda: float = 0.95, clip_range: float = 0.2,
                  clip_range_vf=None, normalize_advantage: bool = True, ent_coef: float = 0.0, vf_coef: float = 0.5,
                  max_grad_norm: float = 0.5, target_kl=None, seed: int | None = None, verbose: int = 0,
-                 policy_kwargs: dict | None = None, device=None, world: int | None = None, rank: int | None = None):
+                 policy_kwargs: dict | None = None, device=None, world: int | None = None, rank: int | None = None,
+                 fused_rollout: bool | None = None):
         if policy != "MlpPolicy":
             raise ValueError("only 'MlpPolicy' (the reference's policy, train.py:126) is provided")
         if clip_range_vf is not None or target_kl is not None:
@@ -115,6 +116,13 @@ class PPO:
             raise NotImplementedError("schedules: the reference uses constant learning_rate / clip_range")
         self.env = env
         self.sim = env.sim
+        # the policy-in-the-loop rollout in one launch (ackphys_ppo_rollout) where the kernels provide
+        # it -- contacts on, the quad mapping, pre-integration observations -- else one act launch and
+        # one step launch per step; both give the same rollout bit for bit
+        can_fuse = self.sim.contacts and self.sim.variant in ("auto", "quad") and not self.sim.poststep_obs
+        if fused_rollout and not can_fuse:
+            raise ValueError("fused_rollout needs contacts, the quad mapping and pre-integration observations")
+        self.fused_rollout = can_fuse if fused_rollout is None else bool(fused_rollout)
         self.device = self.sim.device
         self.n_envs = self.sim.n
         self.learning_rate, self.n_steps, self.batch_size, self.n_epochs = learning_rate, n_steps, batch_size, n_epochs
@@ -212,6 +220,31 @@ class PPO:
         if not self._last_obs_ready:
             self.env.reset()
             self._last_obs_ready = True
+        if self.fused_rollout:
+            self._collect_fused()
+        else:
+            self._collect_per_step()
+        _lib.ppo_check(L.ackppo_gae(_ptr(self.buf_rew), _ptr(self.buf_val), _ptr(self.buf_start),
+                                    _ptr(self.last_values), _ptr(self.last_dones), self.n_steps, N, self.gamma,
+                                    self.gae_lambda, _ptr(self.buf_adv), _ptr(self.buf_ret), s), "ackppo_gae")
+
+    def _collect_fused(self):
+        """The whole rollout as one ackphys_ppo_rollout launch (include/ackphys.h)."""
+        sim, c = self.sim, self.sim._c
+        self.buf_start[0].copy_(self.last_dones)
+        rc = _lib.lib().ackphys_ppo_rollout(
+            sim._ctx, _ptr(self.params), self.n_steps, self._rollout_step, self.seed, 0, self.gamma, c["state"],
+            c["obs_soa"], c["reward"], c["term"], c["trunc"], c["terminal_obs_soa"], c["episode"], _ptr(self.buf_obs),
+            _ptr(self.buf_act), _ptr(self.buf_logp), _ptr(self.buf_val), _ptr(self.buf_rew), _ptr(self.buf_start),
+            _ptr(self.last_dones), _ptr(self.last_values), sim.flags | 2, sim.seed, self._stream())
+        if rc:
+            _lib.check(rc, "ackphys_ppo_rollout")
+        self._rollout_step += self.n_steps
+        self.num_timesteps += self.n_steps * self.n_envs * self.world
+
+    def _collect_per_step(self):
+        """One ackppo_act(_boot) launch and one ackphys_step launch per rollout step."""
+        L, s, N, sim = self.L, self._stream(), self.n_envs, self.sim
         # episode starts: step t's done flags are step t + 1's starts, so the bootstrap writes them
         # straight into buf_start[t + 1] (the last step's into last_dones): one copy per rollout
         self.buf_start[0].copy_(self.last_dones)
@@ -236,9 +269,6 @@ class PPO:
         self.num_timesteps += self.n_steps * N * self.world
         _lib.ppo_check(L.ackppo_value(_ptr(self.params), _ptr(sim.obs_soa), N, _ptr(self.last_values), s),
                        "ackppo_value")
-        _lib.ppo_check(L.ackppo_gae(_ptr(self.buf_rew), _ptr(self.buf_val), _ptr(self.buf_start),
-                                    _ptr(self.last_values), _ptr(self.last_dones), self.n_steps, N, self.gamma,
-                                    self.gae_lambda, _ptr(self.buf_adv), _ptr(self.buf_ret), s), "ackppo_gae")
 
     def train(self):
         L, s = self.L, self._stream()

@@ -84,10 +84,10 @@ def test_rebuild_check_covers_every_included_source():
     """The staleness check of _lib.build() sees every file the kernels #include (the obstacle-scene
     .inc and generated headers included), so an edit to any of them triggers a rebuild."""
     names = {os.path.basename(s) for s in _lib.SOURCES}
-    assert {"ackphys_step.hip", "ackphys_quad.inc", "ackphys_scene.inc", "ackphys_model_gen.h",
-            "ackphys_scene_gen.h", "ackphys.h", "ackphys_model.h"} <= names
+    assert {"ackphys_step.hip", "ackphys_quad.inc", "ackphys_scene.inc", "ackphys_ppo.inc", "ackppo_math.inc",
+            "ackphys_model_gen.h", "ackphys_scene_gen.h", "ackphys.h", "ackphys_model.h", "ackppo.h"} <= names
     assert os.path.basename(_lib.SOURCES[0]) == "ackphys_step.hip"
-    assert {os.path.basename(s) for s in _lib.PPO_SOURCES} == {"ackppo.hip", "ackppo.h"}
+    assert {os.path.basename(s) for s in _lib.PPO_SOURCES} == {"ackppo.hip", "ackppo.h", "ackppo_math.inc"}
 
 
 def test_create_rejects_wrong_blob():

@@ -10,7 +10,8 @@ python3 - "$T" <<'PY'
 import collections, re, sys
 s = open(sys.argv[1]).read()
 for k in ("ackphys_step_nc_kernel", "ackphys_step_quad_kernel", "ackphys_step_obst_kernel",
-          "ackphys_rollout_nc_kernel", "ackphys_rollout_quad_kernel", "ackphys_rollout_obst8_kernel"):
+          "ackphys_rollout_nc_kernel", "ackphys_rollout_quad_kernel", "ackphys_rollout_obst8_kernel",
+          "ackphys_ppo_rollout_quad_kernel", "ackphys_ppo_rollout_obst8_kernel"):
     i = s.find("\n" + k + ":"); j = s.index(".Lfunc_end", i)
     ops = [l.split()[0] for l in s[i:j].split("\n") if l.startswith("\t") and l.strip() and not l.strip().startswith((".", ";"))]
     c = collections.Counter(ops)
