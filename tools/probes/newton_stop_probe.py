@@ -101,7 +101,8 @@ def main():
     st = np.zeros((n, 44))
     o.reset(st, seed=3)
     rng = np.random.default_rng(0)
-    rules = [("exact", 0.0), ("warm", 0.0), ("smooth", 0.0)]
+    rules = [("exact", 0.0), ("warm", 0.0), ("smooth", 0.0), ("warm2", 0.0), ("best3", 0.0)]
+    warm_prev = np.zeros((n, 12))  # qacc of step k - 2 (the steering servo's limit cycle has period 2)
     its = {r: [] for r in rules}
     errs = {r: [] for r in rules}
     for k in range(a.steps):
@@ -133,14 +134,17 @@ def main():
                         elif xx < 0: c += 0.5 * DD * xx * xx
                     return c
                 start = warm if cost(warm) < cost(a0) else a0
+                w2 = warm_prev[e]
+                best3 = min((warm, w2, a0), key=cost)
                 for r in rules:
-                    s0 = warm if r[0] == "warm" else (a0 if r[0] == "smooth" else start)
+                    s0 = {"warm": warm, "smooth": a0, "warm2": w2, "best3": best3}.get(r[0], start)
                     x, itn = solve(M, a0, J, aref, typ, D, R, fl, s0, r[0], r[1],
                                    maxit=int(r[1]) if r[0] == "cap" else 30)
                     row_its[r][e] = itn
                     errs[r].append(np.abs(x - d["qacc"]).max() * DT)
             for r in rules:
                 its[r].append(row_its[r])
+        warm_prev = st[:, 25:37].copy()
         o.step(st, act, flags=FLAG_CONTACTS | FLAG_AUTORESET, seed=3)
     # dual start: the iterations a solver racing both starts would need (the first to converge)
     mn = np.concatenate([np.minimum(a, b) for a, b in zip(its[("warm", 0.0)], its[("smooth", 0.0)])])
