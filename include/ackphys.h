@@ -75,6 +75,16 @@ typedef struct ackphys_env_params {
   double collision_threshold;
   double max_linear_velocity;
   double max_angular_velocity;
+  /* Opt-in task variants, NOT the reference env (1 / 0 = ackermann_env.py exactly):
+   * action_repeat: mj_steps per env step with the same ctrl (observation, reward and done at the
+   *   last one's pre-integration pose; step_count and truncation count env steps; info bad_state
+   *   reports the last mj_step's starting state, a NaN reset by an earlier one is not flagged);
+   *   > 1 runs on the quad mapping (or the obstacle scene) with pre-integration observations;
+   * nohit_clear: a rangefinder reading -1 (no hit) counts as no obstacle in the collision test
+   *   (the reference's min over the readings makes every no-hit ray a collision,
+   *   ackermann_env.py:279-284); info min_lidar is then the minimum over the hits, -1 if none. */
+  int32_t action_repeat;
+  int32_t nohit_clear;
 } ackphys_env_params;
 int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
 

@@ -103,7 +103,21 @@ constexpr float MINVAL = 1e-15f;
 struct EnvParams {
   int max_episode_steps;
   float goal_distance_threshold, collision_threshold, max_linear_velocity, max_angular_velocity;
+  // opt-in task variants (NOT the reference; default off = ackermann_env.py exactly): action_repeat
+  // mj_steps per env step with the same ctrl (obs/reward at the last one's pre-integration pose),
+  // nohit_clear: a rangefinder reading -1 (no hit) is no obstacle for the collision test
+  int action_repeat = 1;
+  int nohit_clear = 0;
 };
+// the collision test's reading of one ray: with nohit_clear a -1 (no hit) reading is +inf
+__device__ __forceinline__ float coll_reading(float v, const EnvParams& prm) {
+  return (prm.nohit_clear && v < 0.0f) ? 3.0e38f : v;
+}
+// min_lidar / collision from the minimum of the collision readings (ackermann_env.py:279-284)
+__device__ __forceinline__ void coll_result(float minl, const EnvParams& prm, float& min_lidar, bool& coll) {
+  coll = minl < prm.collision_threshold;
+  min_lidar = (prm.nohit_clear && minl >= 3.0e38f) ? -1.0f : minl;
+}
 
 struct Args {
   const float* action;
@@ -477,7 +491,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
   if (SC == 0 && __builtin_amdgcn_ballot_w64(!floor_rays_all_miss(p, R)) == 0ull) {
 #pragma unroll
     for (int i = RFIRST; i < 72; i++) stf(dst, i, vo, -1.0f);
-    minl = -1.0f;
+    minl = coll_reading(-1.0f, prm);
   } else {
 #pragma unroll
     for (int i = RFIRST; i < 72; i++) {
@@ -485,7 +499,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
       if constexpr (SC == 0) v = ray_floor_f(F, RAY_DIR[i][0], RAY_DIR[i][1]);
       else v = ray_scene<SC>(F, RAY_DIR[i][0], RAY_DIR[i][1]);
       stf(dst, i, vo, v);
-      minl = fminf(minl, v);
+      minl = fminf(minl, coll_reading(v, prm));
       v71 = v;
     }
   }
@@ -495,8 +509,7 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
 #pragma unroll
   for (int k = 0; k < 7; k++) stf(dst, 72 + k, vo, head[k]);
   if constexpr (RFIRST > 10) minl = fminf(minl, premin());
-  o.minl = minl;
-  o.coll = minl < prm.collision_threshold;
+  coll_result(minl, prm, o.minl, o.coll);
   float r = 0.0f;
   r -= o.dist * 0.1f;
   if (o.term) r += 100.0f;
@@ -2635,13 +2648,13 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
       if (__builtin_amdgcn_ballot_w64(!floor_rays_all_miss(p, R)) == 0ull) {
 #pragma unroll
         for (int i = 10; i < AK_PREP_RAYS; i++) stf(obs, i, vo, -1.0f);
-        mn = -1.0f;
+        mn = coll_reading(-1.0f, A.prm);
       } else {
 #pragma unroll
         for (int i = 10; i < AK_PREP_RAYS; i++) {
           const float v = ray_floor_f(F, RAY_DIR[i][0], RAY_DIR[i][1]);
           stf(obs, i, vo, v);
-          mn = fminf(mn, v);
+          mn = fminf(mn, coll_reading(v, A.prm));
         }
       }
     }
@@ -2869,8 +2882,10 @@ int ackphys_destroy(ackphys_t* ctx) {
 int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* p) {
   if (!ctx || !p) return fail(ACKPHYS_EINVAL, "ackphys_set_env_params: NULL argument");
   if (p->max_episode_steps <= 0) return fail(ACKPHYS_EINVAL, "max_episode_steps must be positive");
+  if (p->action_repeat < 1 || p->action_repeat > 1000) return fail(ACKPHYS_EINVAL, "action_repeat must be in [1, 1000]");
   ctx->prm = ak::EnvParams{p->max_episode_steps, (float)p->goal_distance_threshold, (float)p->collision_threshold,
-                           (float)p->max_linear_velocity, (float)p->max_angular_velocity};
+                           (float)p->max_linear_velocity, (float)p->max_angular_velocity, p->action_repeat,
+                           p->nohit_clear ? 1 : 0};
   return ACKPHYS_OK;
 }
 
@@ -2965,6 +2980,8 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
   // contacts the replicated serial core dominates and one lane per env is marginally faster.
   const bool quad = ctx->variant == ACKPHYS_VARIANT_QUAD ||
                     (ctx->variant == ACKPHYS_VARIANT_AUTO && (flags & ACKPHYS_CONTACTS));
+  if (ctx->prm.action_repeat > 1 && (!(quad || ctx->scene == 1) || (flags & ACKPHYS_POSTSTEP_OBS)))
+    return fail(ACKPHYS_EINVAL, "action_repeat > 1 runs on the quad mapping with pre-integration observations");
   if (ctx->scene == 1) {  // the obstacle scene is specialised on the quad mapping only
     if (ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
       return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");

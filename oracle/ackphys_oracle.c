@@ -88,6 +88,9 @@ struct or_ctx {
   /* AckermannRobotEnv.__init__ kwargs (ackermann_env.py:51-60) */
   int max_steps;
   double goal_thresh, coll_thresh, max_lin, max_ang;
+  /* opt-in task variants (NOT the reference; 1 / 0 = ackermann_env.py): mj_steps per env step,
+     rangefinder -1 readings ignored by the collision test (include/ackphys.h) */
+  int action_repeat, nohit_clear;
   /* resolved ids (reference looks these up by name) */
   int chassis_body, act_steer, act_rl, act_rr;
   int lidar_adr[72];
@@ -357,6 +360,7 @@ int or_create(const void* blob, size_t nbytes, or_ctx** out) {
   c->maxiter = c->m->iterations;
   c->chassis_body = c->m->jnt_bodyid[0]; /* the free joint's body ("chassis") */
   c->max_steps = 1000; c->goal_thresh = 0.5; c->coll_thresh = 0.15; c->max_lin = 1.0; c->max_ang = 1.0;
+  c->action_repeat = 1; c->nohit_clear = 0;
   /* BicycleController actuator lookup by name (controller.py:94-96): steering servo on the
      first limited hinge, rear drives on the first two hinges -- resolved by trnid order. */
   c->act_steer = 0; c->act_rl = 1; c->act_rr = 2;
@@ -386,6 +390,10 @@ void or_set_solver(or_ctx* c, double tolerance, int maxiter) { c->tolerance = to
 void or_set_env_offset(or_ctx* c, int off) { c->env_offset = off; }
 void or_set_env_params(or_ctx* c, int max_steps, double goal, double coll, double max_lin, double max_ang) {
   c->max_steps = max_steps; c->goal_thresh = goal; c->coll_thresh = coll; c->max_lin = max_lin; c->max_ang = max_ang;
+}
+void or_set_env_variant(or_ctx* c, int action_repeat, int nohit_clear) {
+  c->action_repeat = action_repeat < 1 ? 1 : action_repeat;
+  c->nohit_clear = nohit_clear != 0;
 }
 
 /* ------------------------------------------------------------------ mj_kinematics */
@@ -1658,9 +1666,11 @@ static void observe(const or_ctx* c, const or_data* d, const double goal[2], con
   double minl = 1e300;
   for (int i = 0; i < 72; i++) {
     double v = d->sensordata[c->lidar_adr[i]];
+    if (c->nohit_clear && v < 0) continue; /* variant: a no-hit reading is no obstacle */
     if (v < minl) minl = v;
   }
   int coll = minl < c->coll_thresh;
+  if (c->nohit_clear && minl == 1e300) minl = -1.0;
   int t = dist < c->goal_thresh;
   double r = 0.0;
   r -= dist * 0.1;
@@ -1732,7 +1742,9 @@ static void env_step(const or_ctx* c, or_data* d, double* st, const float* actio
   d->ctrl[c->act_steer] = ctrl[0];
   d->ctrl[c->act_rl] = ctrl[1];
   d->ctrl[c->act_rr] = ctrl[2];
-  mj_step(c, d, flags);
+  /* action_repeat mj_steps with the same ctrl (1 = the reference); the observation below comes from
+     the last one's forward pass (its pre-integration pose), as after a single mj_step */
+  for (int s = 0; s < c->action_repeat; s++) mj_step(c, d, flags);
   if (flags & FLAG_POSTSTEP_OBS) { /* mj_forward's position stage on the integrated state feeds the obs */
     kinematics(c, d);
     com_pos(c, d);

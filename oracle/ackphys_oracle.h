@@ -22,6 +22,9 @@ void or_destroy(or_ctx* ctx);
 void or_set_env_offset(or_ctx* ctx, int env_offset);
 void or_set_env_params(or_ctx* ctx, int max_episode_steps, double goal_distance_threshold,
                       double collision_threshold, double max_linear_velocity, double max_angular_velocity);
+/* opt-in task variant (not the reference): action_repeat mj_steps per env step; nohit_clear != 0
+ * ignores -1 (no-hit) rangefinder readings in the collision test (include/ackphys.h) */
+void or_set_env_variant(or_ctx* ctx, int action_repeat, int nohit_clear);
 
 /* ackphys_step on host buffers (flags: ACKPHYS_CONTACTS | ACKPHYS_AUTORESET | ACKPHYS_POSTSTEP_OBS).
  * terminal_obs, info, episode may be NULL. nthreads <= 0: OpenMP default. */

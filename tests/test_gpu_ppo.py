@@ -338,6 +338,32 @@ def test_fused_epoch_matches_per_minibatch_calls():
     assert out[0][2:] == out[1][2:]
 
 
+@pytest.mark.parametrize("variant", [{}, {"action_repeat": 5, "nohit_clear": True}])
+def test_obstacle_scene_ppo_4096(variant):
+    """PPO on the obstacle scene at the bench's per-GPU shape (4096 envs; the fused rollout in the obst8
+    kernel), the fused epoch and the per-minibatch calls (the data-parallel path's kernels) bit-equal,
+    with the reference task and with the opt-in learnable variant."""
+    from mujoco_playground_amd.rl import AckermannVecEnv
+    from mujoco_playground_amd.rl.ppo import PPO
+    out = []
+    for fused in (True, False):
+        venv = AckermannVecEnv(4096, device=DEV, seed=4, contacts=True, scene="obstacles", max_episode_steps=24,
+                               **variant)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=8192, n_epochs=2, seed=5, ent_coef=0.01)
+        assert model.fused_rollout
+        model.fused_epoch = fused
+        model.learn(total_timesteps=3 * 16 * 4096)
+        assert torch.isfinite(model.params).all()
+        lg = model.logger
+        assert np.isfinite(lg["train/value_loss"]) and np.isfinite(lg["train/policy_gradient_loss"])
+        assert lg["rollout/episodes_total"] >= 4096   # truncation at 24 steps within 48
+        out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
+                    lg["train/value_loss"], lg["train/approx_kl"], lg["rollout/ep_rew_mean"]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert out[0][2:] == out[1][2:]
+
+
 def _ppo_rank(rank, world, port, q):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),

@@ -1,0 +1,206 @@
+"""GPU parity of the opt-in task variant (NOT the reference env; include/ackphys.h
+ackphys_env_params.action_repeat / nohit_clear) -- the learnable setting the PPO training log in
+profiles/train/ runs on.
+
+* one R-repeat step == R reference-semantics steps bit for bit (state, observation, reward, info);
+* teacher-forced steps against the f64 oracle set to the same variant (tests/test_oracle_variant.py
+  pins the oracle's variant to its reference-semantics path), flat scene on both mappings and the
+  obstacle scene, with the parity tolerances and excuses of tests/test_gpu_parity.py /
+  tests/test_gpu_obstacles.py;
+* the multi-step launch (ackphys_rollout) equals step-by-step launches bit for bit with
+  action_repeat > 1 (barrier S on the observation wave), including resets and poisoned states;
+* the fused PPO rollout equals the per-step PPO path bit for bit with the variant on;
+* the refusals: action_repeat > 1 on the lane mapping or with post-step observations.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import f64_state
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _sim(n, **kw):
+    from mujoco_playground_amd.sim import BatchedAckermannSim
+    return BatchedAckermannSim(n, DEV, **kw)
+
+
+def _oracle(blob, **params):
+    from oracle.oracle import Oracle
+    o = Oracle(blob)
+    o.set_env_params(**params)
+    return o
+
+
+@pytest.mark.parametrize("scene,contacts,repeat", [("flat", True, 4), ("flat", False, 5), ("obstacles", True, 3)])
+def test_repeat_step_is_repeated_reference_steps(scene, contacts, repeat):
+    """The primary pin: one env step at action_repeat R leaves the physics state (qpos, qvel, warm start)
+    bit-identical to R reference-semantics GPU steps with the same action, and its observation and
+    reward are those of the R-th (the last mj_step's pre-integration pose). The reference-semantics
+    step is held to the oracle by tests/test_gpu_parity.py and tests/test_gpu_obstacles.py."""
+    n, steps = 257, 6
+    kw = dict(seed=8, contacts=contacts, variant="quad", scene=scene, max_episode_steps=1000, nohit_clear=True)
+    a, b = _sim(n, action_repeat=repeat, **kw), _sim(n, **kw)
+    a.reset()
+    b.reset()
+    acts = a.random_actions(steps, seed=8)
+    for k in range(steps):
+        a.step(acts[k], autoreset=False)
+        for _ in range(repeat):
+            b.step(acts[k], autoreset=False)
+        assert torch.equal(a.state[:37], b.state[:37]), f"step {k}: state differs"
+        assert torch.equal(a.obs_soa, b.obs_soa), f"step {k}: obs differs"
+        assert torch.equal(a.reward, b.reward) and torch.equal(a.info, b.info), f"step {k}"
+    assert int(a.state[42].view(torch.int32)[0]) == steps
+    assert int(b.state[42].view(torch.int32)[0]) == steps * repeat
+
+
+# R mj_steps per comparison: the per-mj_step tolerances of the reference-semantics parity tests, R times
+# (the f32 - f64 difference compounds over the substeps; the bit-identity above is the exact pin)
+@pytest.mark.parametrize("variant,contacts,repeat,nohit", [("quad", True, 4, True), ("quad", True, 3, False),
+                                                           ("quad", False, 5, True), ("lane", True, 1, True),
+                                                           ("lane", False, 1, True)])
+def test_variant_teacher_forced_flat(blob, variant, contacts, repeat, nohit, monkeypatch):
+    import test_gpu_parity as P
+    from test_gpu_parity import teacher_forced
+    monkeypatch.setattr(P, "TOL_QPOS", P.TOL_QPOS * repeat)
+    monkeypatch.setattr(P, "TOL_QVEL", P.TOL_QVEL * repeat)
+    n, steps, seed = 192, 40, 17
+    kw = dict(max_episode_steps=25, action_repeat=repeat, nohit_clear=nohit)
+    sim = _sim(n, seed=seed, contacts=contacts, variant=variant, **kw)
+    sim.reset()
+    acts = sim.random_actions(steps, seed=seed)
+    w = teacher_forced(sim, _oracle(blob, **kw), acts, steps, (1 if contacts else 0) | 2, seed)
+    print("worst", variant, contacts, repeat, nohit, w)
+    minl, coll = sim.info[0], sim.info[1] > 0
+    if nohit:  # a -1 (no hit) is no obstacle: collision iff a real hit is under the threshold
+        assert torch.equal(coll, (minl >= 0) & (minl < 0.15))
+    else:
+        assert torch.equal(coll, minl < 0.15)
+
+
+def test_variant_differs_from_reference_step(blob):
+    """action_repeat really integrates R mj_steps: driving straight ahead, R=4 env steps cover about
+    four times the distance of reference steps."""
+    n, steps = 64, 60
+    a, b = _sim(n, seed=2, action_repeat=4), _sim(n, seed=2)
+    a.reset()
+    b.reset()
+    x0 = a.state[:2].clone()
+    act = torch.tensor([[1.0, 0.0]], device=DEV).expand(n, 2).contiguous()
+    for _ in range(steps):
+        a.step(act, autoreset=False)
+        b.step(act, autoreset=False)
+    da = (a.state[:2] - x0).norm(dim=0)
+    db = (b.state[:2] - x0).norm(dim=0)
+    assert float(db.min()) > 0.0
+    assert float((da / db).min()) > 2.5, (da / db).min()
+
+
+def test_variant_teacher_forced_obstacles(monkeypatch):
+    from mujoco_playground_amd import _lib
+    import test_gpu_obstacles as T
+    monkeypatch.setattr(T, "TOL_QPOS", T.TOL_QPOS * 3)
+    monkeypatch.setattr(T, "TOL_QVEL", T.TOL_QVEL * 3)
+    # the observed pose is the f64 oracle's after 2 mj_steps, ~1e-6 from the kernel's f32 one
+    monkeypatch.setattr(T, "HORIZ_TOL", 1e-5)
+    sblob = _lib.load_blob("obstacles")
+    lo, hi = _boxes(sblob)
+    rng = np.random.default_rng(9)
+    n, steps = 256, 40
+    st = T.wall_states(n, lo, hi, rng)
+    kw = dict(action_repeat=3, nohit_clear=True)
+    sim = _sim(n, seed=9, scene="obstacles", **kw)
+    sim.set_state(T.to_device(st))
+    gen = torch.Generator(device="cpu").manual_seed(9)
+    acts = []
+    for _ in range(steps):
+        x = torch.rand(n, 2, generator=gen) * 2 - 1
+        x[:, 0] = 0.4 + 0.6 * torch.rand(n, generator=gen)
+        acts.append(x.to(DEV))
+    pre = _oracle(sblob, action_repeat=2)
+
+    def seen(before, act):  # the observed pose: after the first R-1 = 2 mj_steps
+        s = before.copy()
+        pre.step(s, act, flags=1, seed=9)
+        return s
+    w = T.teacher_forced(sim, _oracle(sblob, **kw), acts, steps, 1 | 2, 9, lo, hi, obs_pose=seen)
+    print("walls R=3", w)
+    assert bool((sim.info[1] > 0).any())   # robots against walls: real collisions are still reported
+
+
+def _boxes(sblob):
+    from mujoco_playground_amd.model import blob as B
+    h = B.unpack_header(sblob)
+    g = [i for i in range(h.ngeom) if h.geom_type[i] == 6]
+    c = np.array([list(h.geom_pos[i]) for i in g])
+    s = np.array([list(h.geom_size[i]) for i in g])
+    return c - s, c + s
+
+
+@pytest.mark.parametrize("scene,contacts", [("flat", True), ("flat", False), ("obstacles", True)])
+def test_variant_rollout_equals_steps(scene, contacts):
+    from mujoco_playground_amd.sim import ST_QVEL
+    n, K = 301, 17
+    kw = dict(seed=3, contacts=contacts, variant="quad", scene=scene, max_episode_steps=7, action_repeat=3,
+              nohit_clear=True)
+    a, b = _sim(n, **kw), _sim(n, **kw)
+    a.reset()
+    b.reset()
+    for s in (a, b):
+        s.state[ST_QVEL + 2, [7, 150]] = float("nan")
+    acts = a.random_actions(K, seed=21)
+    obs, rew, term, trunc = a.rollout(acts)
+    info = a.last_rollout["info"]
+    for k in range(K):
+        ob, rb, tb, trb = b.step(acts[k])
+        assert torch.equal(obs[k], ob), f"obs differs at step {k}"
+        assert torch.equal(rew[k], rb) and torch.equal(term[k], tb) and torch.equal(trunc[k], trb), k
+        assert torch.equal(info[k], b.info), f"info differs at step {k}"
+    assert torch.equal(a.state, b.state)
+    assert torch.equal(a.episode, b.episode)
+    # the poisoned envs were reset to qpos0 by the first mj_step (info[3], bad_state, reports the last
+    # mj_step's starting state at action_repeat > 1: include/ackphys.h)
+    assert bool(torch.isfinite(a.state[:37, [7, 150]]).all())
+
+
+@pytest.mark.parametrize("scene", ["flat", "obstacles"])
+def test_variant_fused_ppo_rollout_equals_per_step(scene):
+    from mujoco_playground_amd.rl import AckermannVecEnv
+    from mujoco_playground_amd.rl.ppo import PPO
+    from test_gpu_ppo_rollout import _compare
+    n, T = 203, 13
+    pair = []
+    for fused in (True, False):
+        venv = AckermannVecEnv(n, device=DEV, seed=5, contacts=True, scene=scene, max_episode_steps=6,
+                               goal_distance_threshold=2.4, action_repeat=4, nohit_clear=True)
+        pair.append(PPO("MlpPolicy", venv, n_steps=T, batch_size=64, n_epochs=1, seed=3, fused_rollout=fused))
+    a, b = pair
+    assert a.fused_rollout and not b.fused_rollout
+    for it in range(2):
+        a.collect_rollouts()
+        b.collect_rollouts()
+        torch.cuda.synchronize()
+        _compare(a, b, f"{scene} R=4 rollout {it}")
+    assert 0 < float(a.buf_start[1:].sum()) < a.buf_start[1:].numel()
+
+
+def test_variant_refusals():
+    a = _sim(16, variant="lane", contacts=True, action_repeat=2)
+    a.reset()
+    with pytest.raises(RuntimeError):
+        a.step(torch.zeros(16, 2, device=DEV))
+    b = _sim(16, variant="quad", contacts=True, action_repeat=2, poststep_obs=True)
+    b.reset()
+    with pytest.raises(RuntimeError):
+        b.step(torch.zeros(16, 2, device=DEV))
+    with pytest.raises((RuntimeError, ValueError)):
+        _sim(16, action_repeat=0)
