@@ -28,6 +28,11 @@
 // layout: [AK_NSTAMP][blocks] phase stamps, [blocks][64] Newton iteration counts, [5][blocks] Newton phases
 #define AK_NSTAMP 24
 __device__ unsigned long long* g_stamps;
+// slot dump of env 0 (quad kernels; tools/probes/quad_slot_probe.py): [4 lanes][QSN_MAX][AK_SLOTF]
+// then qacc_smooth[12], qacc[12]
+#define AK_SLOTF 40
+#define AK_QSN_MAX 12
+__device__ float* g_dump;
 // The stamps are kept in LDS (one row per wave) and written out when the wave leaves its role
 // function: a global store per stamp would add a pointer load and a vmcnt(0) wait to every stamp.
 __shared__ unsigned long long ak_stamp_lds[4][AK_NSTAMP];
@@ -2833,6 +2838,10 @@ const char* ackphys_last_error(void) { return g_err; }
 #ifdef AK_STAMPS
 int ackphys_diag_set_stamps(void* buf) {
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf));
+  return e == hipSuccess ? 0 : hipfail(e, "hipMemcpyToSymbol");
+}
+int ackphys_diag_set_dump(void* buf) {
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_dump), &buf, sizeof(buf));
   return e == hipSuccess ? 0 : hipfail(e, "hipMemcpyToSymbol");
 }
 #endif

@@ -798,6 +798,7 @@ static int plane_convex(const or_ctx* c, const or_data* d, int g1, int g2, doubl
    deepest point moved half the penetration back (the witness midpoint). Support points that are
    not unique (face/edge parallel to the separating plane) average the candidates within 1 um. */
 #define OR_TIE 1e-6
+#define OR_KINK_TOL 5e-7
 static void box_frame(const or_data* d, const apm_model_t* m, int g, double c[3], double A[3][3], double h[3]) {
   for (int k = 0; k < 3; k++) {
     c[k] = d->geom_xpos[g][k];
@@ -909,6 +910,19 @@ static void edge_family(const double cc[3], const double a[3], double r, double 
   }
   double phi = 0.5 * (lo + hi);
   for (int t = 0; t < 3; t++) n_out[t] = cos(phi) * u[t] + sin(phi) * w[t];
+  /* the family's kink: the cylinder extent h|a.n| + r sqrt(1 - (a.n)^2) has a corner at a.n = 0
+     (n = +-a x A[k], a wheel rim against a box edge) where the separation peaks; the search above
+     only brackets it, so snap to it when it is as good to within OR_KINK_TOL (the kernel's f32
+     search is rounding-limited there; both apply this rule, ackphys_scene.inc cb_edge_family) */
+  double nk[3];
+  cross3(nk, a, A[k]);
+  double len = sqrt(dot3(nk, nk));
+  if (len >= 1e-6) {
+    double il = (dot3(nk, n_out) < 0 ? -1.0 : 1.0) / len;
+    for (int t = 0; t < 3; t++) nk[t] *= il;
+    if (cyl_box_sep(cc, a, r, h, bc, A, bh, nk, &sg) >= cyl_box_sep(cc, a, r, h, bc, A, bh, n_out, &sg) - OR_KINK_TOL)
+      memcpy(n_out, nk, sizeof nk);
+  }
 }
 /* can an edge of the box parallel to axis k come within rb of point c? */
 static int edge_reach(const double c[3], const double bc[3], const double A[3][3], const double bh[3], int k, double rb) {

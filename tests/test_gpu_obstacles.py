@@ -219,9 +219,10 @@ def _horizontal(before_e, ray, g, r):
     return abs(d[2]) <= HORIZ_TOL * np.linalg.norm(d) and abs(pair[0] + 1.0) <= 1e-6 and abs(pair[1] - 12.0) <= 1e-4
 
 
-def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None):
+def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None, excuse=None):
     """obs_pose(before, actions) -> the states the observations are taken at (default: `before`, the
-    pre-integration pose; with action_repeat R, the pose after R-1 mj_steps)."""
+    pre-integration pose; with action_repeat R, the pose after R-1 mj_steps). excuse(k, e, before_e,
+    act_e, after_e) replaces the boundary excuse (default: _excused with the oracle `o`)."""
     worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0, excused=0, grazing_rays=0, rays=0)
     for k in range(steps):
         before = f64_state(sim.state)
@@ -236,7 +237,9 @@ def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None):
         dv = np.abs(after[:, 13:25] - ref[:, 13:25]).max(axis=1)
         ok = (dq <= TOL_QPOS) & (dv <= TOL_QVEL)
         for e in np.nonzero(~ok)[0]:
-            assert _excused(o, before[e], a_np[e], after[e], flags, seed), (
+            ex = (excuse(k, e, before[e], a_np[e], after[e]) if excuse is not None
+                  else _excused(o, before[e], a_np[e], after[e], flags, seed))
+            assert ex, (
                 f"step {k} env {e}: |dqpos| {dq[e]:.3e} |dqvel| {dv[e]:.3e}")
             worst["excused"] += 1
         worst["qpos"] = max(worst["qpos"], dq[ok].max(initial=0.0))
@@ -330,3 +333,29 @@ def test_obstacle_wall_contacts(sblob, boxes):
         c = o.contacts(fin[e, :13])
         nbox += int(((c[:, 0] > 0) & (c[:, 2] < 0)).sum())
     assert nbox >= 20, nbox
+
+
+def test_wheel_on_box_edge_kink(sblob):
+    """A recorded state (tests/golden/edge_kink_state.npz, from the action-repeat parity run): a front
+    wheel's rim pressed on a vertical box edge, wheels spinning. The best separating direction is the
+    kink of the edge family (n = a x e_z, a.n = 0), where the witness sits mid-rim; the f32 search had
+    landed ~5e-5 rad off it, flipped the cap-side tie and moved the contact point by the half-width
+    (|dqvel| 0.18 against the oracle). Both sides now snap to the kink (cb_edge_family / edge_family)."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "edge_kink_state.npz"))
+    before, action = d["before"], d["action"].reshape(1, 2)
+    o = oracle(sblob)
+    c = o.contacts(before[:13])
+    box = c[(c[:, 0] >= 41) & (c[:, 1] < 41)]   # wheel (41-44) vs box
+    assert len(box) == 1 and abs(box[0, 2]) > 1e-4   # one wheel-box contact, 0.45 mm deep
+    ref = before[None].copy()
+    o.step(ref, action, flags=1, seed=9)
+    for variant_n in (1, 37):   # alone, and inside a wave of other envs
+        sim = make_sim(variant_n, seed=9)
+        st = np.repeat(before[None], variant_n, axis=0)
+        sim.set_state(to_device(st))
+        sim.step(torch.tensor(np.repeat(action, variant_n, axis=0), device=DEV), autoreset=False)
+        torch.cuda.synchronize()
+        after = f64_state(sim.state)
+        assert np.abs(after[:, :13] - ref[0, :13]).max() <= TOL_QPOS
+        assert np.abs(after[:, 13:25] - ref[0, 13:25]).max() <= TOL_QVEL

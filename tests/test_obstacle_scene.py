@@ -205,3 +205,29 @@ def test_ray_box_matches_slab_reference(scene):
             assert abs(got - ref) < 1e-9, (got, ref)
             hits += np.isfinite(tb) and tb < tfl
     assert hits > 100
+
+
+def test_edge_family_kink_witness():
+    """Oracle side of the edge-kink rule (tests/golden/edge_kink_state.npz): the wheel-box contact's
+    normal is perpendicular to the wheel axis to rounding, so the witness is mid-rim (the cap-side
+    tie), i.e. the contact point lies in the wheel's mid-plane."""
+    import os
+    from mujoco_playground_amd import _lib
+    from mujoco_playground_amd.model import compiler as Cm
+    from mujoco_playground_amd.model.mathutil import quat_to_mat
+    from oracle.oracle import Oracle
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "edge_kink_state.npz"))
+    c = Oracle(_lib.load_blob("obstacles")).contacts(d["before"][:13])
+    box = c[(c[:, 0] >= 41) & (c[:, 1] < 41)]
+    assert len(box) == 1
+    n = box[0, 6:9]
+    if not os.path.exists(Cm.obstacle_scene_path()):
+        pytest.skip("reference MJCF not present")
+    m = Cm.compile_scene(Cm.obstacle_scene_path(), Cm.default_model_path())
+    xpos, xmat, _, _, _ = Cm.body_frames(m, d["before"][:13])
+    g = int(box[0, 0])
+    b = m.geom_bodyid[g]
+    a = (xmat[b] @ quat_to_mat(m.geom_quat[g]))[:, 2]
+    centre = xpos[b] + xmat[b] @ m.geom_pos[g]
+    assert abs(a @ n) < 1e-9
+    assert abs(a @ (box[0, 3:6] - centre)) < 1e-9   # mid-plane witness

@@ -1,4 +1,5 @@
-"""Debug probe: dump the state/obs of the first obstacle-scene R=3 ray mismatch (test_gpu_variant)."""
+"""Debug probe: dump the state of an obstacle-scene R=3 step that misses the oracle (test_gpu_variant)
+with the GPU's R=1 chain from the same state."""
 import os
 import sys
 
@@ -9,9 +10,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests"))
 from conftest import f64_state  # noqa: E402
 import test_gpu_obstacles as T  # noqa: E402
-from test_gpu_variant import _boxes, _oracle, _sim  # noqa: E402
+from test_gpu_variant import _boxes, _sim  # noqa: E402
 from mujoco_playground_amd import _lib  # noqa: E402
 
+K, E = int(sys.argv[1]), int(sys.argv[2])
 sblob = _lib.load_blob("obstacles")
 lo, hi = _boxes(sblob)
 rng = np.random.default_rng(9)
@@ -26,21 +28,27 @@ for _ in range(steps):
     x = torch.rand(n, 2, generator=gen) * 2 - 1
     x[:, 0] = 0.4 + 0.6 * torch.rand(n, generator=gen)
     acts.append(x.to("cuda:0"))
-o = _oracle(sblob, **kw)
-for k in range(14):
+for k in range(K + 1):
     before = f64_state(sim.state)
     sim.step(acts[k], autoreset=True)
     torch.cuda.synchronize()
-    after = f64_state(sim.state)
-ref = before.copy()
-a_np = acts[13].cpu().numpy()
-oobs, *_ = o.step(ref, a_np, flags=3, seed=9)
-# the GPU's own pose after 2 mj_steps: an R=2 sim from `before`
-s2 = _sim(n, seed=9, scene="obstacles", action_repeat=2, nohit_clear=True)
-s2.set_state(T.to_device(before))
-s2.step(acts[13], autoreset=False)
-torch.cuda.synchronize()
-mid_gpu = f64_state(s2.state)
-np.savez("gpurun_out/variant_ray_probe.npz", before=before, after=after, ref=ref, act=a_np,
-         gobs=sim.obs_soa.cpu().numpy().T, oobs=oobs, mid_gpu=mid_gpu)
-print("saved", np.abs(sim.obs_soa.cpu().numpy().T[5, 30] - oobs[5, 30]))
+after = f64_state(sim.state)
+chain = [before[E].copy()]
+for nsim in (1, 256):   # a 1-env shadow and a full-width R=1 sim from the same states
+    s1 = _sim(nsim, seed=9, scene="obstacles", nohit_clear=True)
+    cur = before.copy()
+    for j in range(3):
+        s1.set_state(T.to_device(cur[:nsim] if nsim > 1 else cur[E:E + 1]))
+        s1.step(acts[K][:nsim] if nsim > 1 else acts[K][E:E + 1], autoreset=False)
+        torch.cuda.synchronize()
+        nx = f64_state(s1.state)
+        if nsim > 1:
+            cur = np.concatenate([nx, cur[nsim:]])
+            chain.append(nx[E].copy())
+        else:
+            cur = cur.copy()
+            cur[E] = nx[0]
+            chain.append(nx[0].copy())
+np.savez("gpurun_out/variant_step_probe.npz", before=before[E], after=after[E], act=acts[K][E].cpu().numpy(),
+         chain=np.array(chain))
+print("saved")
