@@ -115,6 +115,14 @@ struct EnvParams {
   int nohit_clear = 0;
 };
 // the collision test's reading of one ray: with nohit_clear a -1 (no hit) reading is +inf
+// the quad kernels compile the variant only into their VAR instantiations (the host launches those
+// whenever a variant field is set); the lane kernels read the fields at run time
+template <bool VAR>
+__device__ __forceinline__ EnvParams var_prm(const EnvParams& p) {
+  EnvParams r = p;
+  if (!VAR) { r.action_repeat = 1; r.nohit_clear = 0; }
+  return r;
+}
 __device__ __forceinline__ float coll_reading(float v, const EnvParams& prm) {
   return (prm.nohit_clear && v < 0.0f) ? 3.0e38f : v;
 }
@@ -2991,6 +2999,20 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
                     (ctx->variant == ACKPHYS_VARIANT_AUTO && (flags & ACKPHYS_CONTACTS));
   if (ctx->prm.action_repeat > 1 && (!(quad || ctx->scene == 1) || (flags & ACKPHYS_POSTSTEP_OBS)))
     return fail(ACKPHYS_EINVAL, "action_repeat > 1 runs on the quad mapping with pre-integration observations");
+  // the task variant on the quad mapping runs in dedicated rollout kernels (K = 1 for a step)
+  if ((ctx->prm.action_repeat > 1 || ctx->prm.nohit_clear) && (quad || ctx->scene == 1) &&
+      !(flags & ACKPHYS_POSTSTEP_OBS)) {
+    if (ctx->scene == 1 && ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
+      return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
+    a.epw = quad_epw(true, ctx->scene);
+    if (ctx->scene == 1 && a.epw > 8) a.epw = 8;  // the 32-lane slot stride holds 8 envs per wave
+    const int blocks = (ctx->n_env + a.epw - 1) / a.epw;
+    hipLaunchKernelGGL(ctx->scene == 1 ? ackphys_rollout_obst8_var_kernel : ackphys_rollout_quad_var_kernel,
+                       dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hipfail(e, "ackphys_rollout_var launch");
+    return ACKPHYS_OK;
+  }
   if (ctx->scene == 1) {  // the obstacle scene is specialised on the quad mapping only
     if (ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
       return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
@@ -3065,7 +3087,9 @@ int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32
   ak::PpoArgs P{params, policy_seed, step0, deterministic, gamma, n_steps, obs_rows, actions, log_prob, value,
                 rollout_reward, episode_starts, last_dones, last_values};
   const int blocks = (ctx->n_env + ak::PPO_PE - 1) / ak::PPO_PE;
-  hipLaunchKernelGGL(ctx->scene == 1 ? ackphys_ppo_rollout_obst8_kernel : ackphys_ppo_rollout_quad_kernel,
+  const bool var = ctx->prm.action_repeat > 1 || ctx->prm.nohit_clear;
+  hipLaunchKernelGGL(ctx->scene == 1 ? (var ? ackphys_ppo_rollout_obst8_var_kernel : ackphys_ppo_rollout_obst8_kernel)
+                                     : (var ? ackphys_ppo_rollout_quad_var_kernel : ackphys_ppo_rollout_quad_kernel),
                      dim3(blocks), dim3(128), 0, (hipStream_t)stream, a, P);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_ppo_rollout launch");
