@@ -62,7 +62,8 @@ def main():
     rew = torch.zeros(n, device=dev)
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nb = (n + 15) // 16 if quad else (n + 63) // 64
+    epw = (8 if ROLL > 1 else 16) if quad else 64  # envs per workgroup of the stamped launch (quad_epw)
+    nb = (n + epw - 1) // epw
     stamps = torch.zeros(NSTAMP * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
     p = lambda t: P(t.data_ptr())
@@ -98,7 +99,7 @@ def main():
                     f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"])))
             its = its[: 64 * nb]
             if quad:
-                its = its.reshape(nb, 64)[:, :16].reshape(-1)
+                its = its.reshape(nb, 64)[:, :epw].reshape(-1)
             if k == 200:
                 ls = its >> 8
                 its = its & 0xFF
