@@ -2978,7 +2978,9 @@ int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* st
 // of 16: contacts on 39.6 -> 37.2 us per step (tools/quad_epw_sweep.sh). The obstacle scene's
 // slot LDS (94 KB at a 64-lane stride) allows one workgroup per CU, so its 8-env rollout kernel
 // lays the slots out at a 32-lane stride (47 KB; ackphys_rollout_obst8_kernel); at 16 envs per
-// wave and 94 KB, 8 envs had measured 84 us. ACKPHYS_QUAD_EPW overrides (experiments).
+// wave and 94 KB, 8 envs had measured 84 us. The flat scene's kernels run split quads (8 lanes per
+// env, QSlots in ackphys_quad.inc): at most 8 envs per wave, per-step launches included.
+// ACKPHYS_QUAD_EPW overrides (experiments; <= 8 on the flat scene).
 static int quad_epw(bool multi, int scene) {
   static int v = -1;
   if (v < 0) {
@@ -2986,6 +2988,7 @@ static int quad_epw(bool multi, int scene) {
     v = s ? atoi(s) : 0;
     if (v < 0 || v > 16) v = 0;
   }
+  if (scene == 0) return v ? (v < 8 ? v : 8) : 8;
   if (!multi) return 16;
   return v ? v : 8;
 }
@@ -3005,7 +3008,7 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
     if (ctx->scene == 1 && ctx->variant != ACKPHYS_VARIANT_QUAD && ctx->variant != ACKPHYS_VARIANT_AUTO)
       return fail(ACKPHYS_EINVAL, "the obstacle scene runs on the quad mapping (variant AUTO or QUAD)");
     a.epw = quad_epw(true, ctx->scene);
-    if (ctx->scene == 1 && a.epw > 8) a.epw = 8;  // the 32-lane slot stride holds 8 envs per wave
+    if (a.epw > 8) a.epw = 8;  // the 32-lane slot stride / split quads hold 8 envs per wave
     const int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     hipLaunchKernelGGL(ctx->scene == 1 ? ackphys_rollout_obst8_var_kernel : ackphys_rollout_quad_var_kernel,
                        dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
