@@ -2978,9 +2978,9 @@ int ackphys_rollout(ackphys_t* ctx, int k_steps, const float* actions, float* st
 // of 16: contacts on 39.6 -> 37.2 us per step (tools/quad_epw_sweep.sh). The obstacle scene's
 // slot LDS (94 KB at a 64-lane stride) allows one workgroup per CU, so its 8-env rollout kernel
 // lays the slots out at a 32-lane stride (47 KB; ackphys_rollout_obst8_kernel); at 16 envs per
-// wave and 94 KB, 8 envs had measured 84 us. The flat scene's kernels run split quads (8 lanes per
-// env, QSlots in ackphys_quad.inc): at most 8 envs per wave, per-step launches included.
-// ACKPHYS_QUAD_EPW overrides (experiments; <= 8 on the flat scene).
+// wave and 94 KB, 8 envs had measured 84 us. Since round 3 both scenes' kernels run split quads (8
+// lanes per env, QSlots in ackphys_quad.inc): at most 8 envs per wave, per-step launches included.
+// ACKPHYS_QUAD_EPW overrides (experiments; <= 8).
 static int quad_epw(bool multi, int scene) {
   static int v = -1;
   if (v < 0) {
@@ -2988,9 +2988,9 @@ static int quad_epw(bool multi, int scene) {
     v = s ? atoi(s) : 0;
     if (v < 0 || v > 16) v = 0;
   }
-  if (scene == 0) return v ? (v < 8 ? v : 8) : 8;
-  if (!multi) return 16;
-  return v ? v : 8;
+  (void)multi;
+  (void)scene;
+  return v ? (v < 8 ? v : 8) : 8;
 }
 
 static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream) {
@@ -3024,8 +3024,7 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_obst_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(!multi ? ackphys_step_obst_kernel
-                                : (a.epw <= 8 ? ackphys_rollout_obst8_kernel : ackphys_rollout_obst_kernel),
+      hipLaunchKernelGGL(!multi ? ackphys_step_obst_kernel : ackphys_rollout_obst8_kernel,
                          dim3(blocks), dim3(128), 0, (hipStream_t)stream, a);
   } else if (quad) {
     a.epw = (flags & ACKPHYS_POSTSTEP_OBS) ? 16 : quad_epw(multi, ctx->scene);

@@ -62,7 +62,7 @@ def main():
     rew = torch.zeros(n, device=dev)
     term = torch.zeros(n, dtype=torch.uint8, device=dev)
     trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
-    epw = (8 if ROLL > 1 else 16) if quad else 64  # envs per workgroup of the stamped launch (quad_epw)
+    epw = 8 if quad else 64  # envs per workgroup of the stamped launch (quad_epw)
     nb = (n + epw - 1) // epw
     stamps = torch.zeros(NSTAMP * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(P(stamps.data_ptr())) == 0
