@@ -82,9 +82,14 @@ typedef struct ackphys_env_params {
    *   > 1 runs on the quad mapping (or the obstacle scene) with pre-integration observations;
    * nohit_clear: a rangefinder reading -1 (no hit) counts as no obstacle in the collision test
    *   (the reference's min over the readings makes every no-hit ray a collision,
-   *   ackermann_env.py:279-284); info min_lidar is then the minimum over the hits, -1 if none. */
+   *   ackermann_env.py:279-284); info min_lidar is then the minimum over the hits, -1 if none;
+ * goal_cells (obstacle scene only, 0 = the reference's goals 2-8 m away in a random direction,
+ *   ackermann_env.py:167-172): > 0 draws each episode's goal at the centre of a box-free maze
+ *   cell 4-connected to the spawn cell within goal_cells breadth-first steps of it (a maze task
+ *   a policy can reach; the reference's goals mostly lie behind walls). */
   int32_t action_repeat;
   int32_t nohit_clear;
+  int32_t goal_cells;
 } ackphys_env_params;
 int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
 

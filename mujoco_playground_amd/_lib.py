@@ -61,7 +61,7 @@ class EnvParams(C.Structure):
                 ("collision_threshold", C.c_double), ("max_linear_velocity", C.c_double),
                 ("max_angular_velocity", C.c_double),
                 # opt-in task variants (NOT the reference; 1 / 0 = ackermann_env.py exactly)
-                ("action_repeat", C.c_int32), ("nohit_clear", C.c_int32)]
+                ("action_repeat", C.c_int32), ("nohit_clear", C.c_int32), ("goal_cells", C.c_int32)]
 
 
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:

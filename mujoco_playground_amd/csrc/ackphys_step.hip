@@ -113,6 +113,9 @@ struct EnvParams {
   // nohit_clear: a rangefinder reading -1 (no hit) is no obstacle for the collision test
   int action_repeat = 1;
   int nohit_clear = 0;
+  // goal_cells > 0 (obstacle scene only): goals at the centres of the spawn-connected free maze
+  // cells within goal_cells breadth-first steps (scene1::FREE_XY / FREE_LE), not 2-8 m away
+  int goal_cells = 0;
 };
 // the collision test's reading of one ray: with nohit_clear a -1 (no hit) reading is +inf
 // the quad kernels compile the variant only into their VAR instantiations (the host launches those
@@ -2052,10 +2055,25 @@ __device__ __forceinline__ void reset_pose(float qpos[13], float qvel[NV], float
 }
 
 // goal = robot_start_position + (d cos th, d sin th) (ackermann_env.py:167-172) in the odometry
-// frame, where the start position is (0, 0) whatever the spawn point (odometry.py:62-103)
-__device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_t episode, float& gx, float& gy) {
+// frame, where the start position is (0, 0) whatever the spawn point (odometry.py:62-103).
+// Opt-in maze task (obstacle scene, prm.goal_cells > 0): the centre of free cell
+// floor(u * FREE_LE[d]) of the breadth-first list, u from the same Philox word, integer arithmetic
+// (the oracle draws the same cell), minus the spawn (odometry frame: the reset pose is identity)
+template <int SC>
+__device__ __forceinline__ void goal_sample(uint64_t seed, int64_t genv, uint32_t episode, const EnvParams& prm,
+                                            float& gx, float& gy) {
   uint32_t c[4] = {(uint32_t)genv, episode, 0u, 0u};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  if constexpr (SC == 1) {
+    if (prm.goal_cells > 0) {
+      using namespace scene1;
+      const uint32_t nle = (uint32_t)FREE_LE[prm.goal_cells < FREE_MAXD ? prm.goal_cells : FREE_MAXD];
+      const uint32_t i = (uint32_t)(((uint64_t)(c[0] >> 8) * nle) >> 24);
+      gx = FREE_XY[i][0] - SPAWN[0];
+      gy = FREE_XY[i][1] - SPAWN[1];
+      return;
+    }
+  }
   float d = 2.0f + 6.0f * u01(c[0]);
   float th = 6.283185307179586f * u01(c[1]);
   gx = d * cosf(th);
@@ -2070,7 +2088,7 @@ __device__ __forceinline__ void reset_env(const Soa& state, const Soa& obs, uint
   float qpos[13], qvel[NV], warm[NV];
   reset_pose<SC>(qpos, qvel, warm);
   float gx, gy;
-  goal_sample(seed, genv, episode, gx, gy);
+  goal_sample<SC>(seed, genv, episode, prm, gx, gy);
   float q[4] = {qpos[3], qpos[4], qpos[5], qpos[6]};
   normq(q);
   float R[9];
@@ -2900,9 +2918,11 @@ int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* p) {
   if (!ctx || !p) return fail(ACKPHYS_EINVAL, "ackphys_set_env_params: NULL argument");
   if (p->max_episode_steps <= 0) return fail(ACKPHYS_EINVAL, "max_episode_steps must be positive");
   if (p->action_repeat < 1 || p->action_repeat > 1000) return fail(ACKPHYS_EINVAL, "action_repeat must be in [1, 1000]");
+  if (p->goal_cells < 0) return fail(ACKPHYS_EINVAL, "goal_cells must be >= 0");
+  if (p->goal_cells > 0 && ctx->scene != 1) return fail(ACKPHYS_EINVAL, "goal_cells needs the obstacle scene (maze cells)");
   ctx->prm = ak::EnvParams{p->max_episode_steps, (float)p->goal_distance_threshold, (float)p->collision_threshold,
                            (float)p->max_linear_velocity, (float)p->max_angular_velocity, p->action_repeat,
-                           p->nohit_clear ? 1 : 0};
+                           p->nohit_clear ? 1 : 0, p->goal_cells};
   return ACKPHYS_OK;
 }
 

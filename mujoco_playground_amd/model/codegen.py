@@ -406,6 +406,25 @@ def hull_features(hv: np.ndarray):
     return np.array(fn), np.array(ed)
 
 
+def maze_free_cells(cells, nx: int, ny: int, x0: float, y0: float, cell: float, spawn) -> list:
+    """Free-cell goals of the opt-in maze task: (centre x, centre y, breadth-first distance in
+    cells) of every box-free grid cell 4-connected to the spawn cell, the spawn cell excluded,
+    sorted by distance, then row, then column."""
+    sx, sy = int(np.floor((spawn[0] - x0) / cell)), int(np.floor((spawn[1] - y0) / cell))
+    _req(0 <= sx < nx and 0 <= sy < ny and not cells[sy * nx + sx], "spawn in a free grid cell")
+    dist = {(sx, sy): 0}
+    todo = [(sx, sy)]
+    for c in todo:  # breadth-first: `todo` grows while it is walked
+        for dx, dy in ((1, 0), (-1, 0), (0, 1), (0, -1)):
+            n = (c[0] + dx, c[1] + dy)
+            if 0 <= n[0] < nx and 0 <= n[1] < ny and not cells[n[1] * nx + n[0]] and n not in dist:
+                dist[n] = dist[c] + 1
+                todo.append(n)
+    out = [(x0 + (ix + 0.5) * cell, y0 + (iy + 0.5) * cell, d, iy, ix) for (ix, iy), d in dist.items() if d > 0]
+    out.sort(key=lambda t: (t[2], t[3], t[4]))
+    return [(x, y, d) for x, y, d, _, _ in out]
+
+
 def generate_scene(ms: CompiledModel, blob_fnv: int, robot: CompiledModel, ns: str = "scene1") -> str:
     """Scene header: the static world the robot is merged into (obstacle scene). The robot part
     of `ms` must compile to exactly the robot header's constants."""
@@ -431,6 +450,7 @@ def generate_scene(ms: CompiledModel, blob_fnv: int, robot: CompiledModel, ns: s
                         and hi[b, 1] > cy0 + eps:
                     cells[iy * nx + ix].append(b)
     ck = max(1, max(len(c) for c in cells))
+    free = maze_free_cells(cells, nx, ny, x0, y0, cell, ms.spawn)
     table = np.full((nx * ny, ck), -1, np.int64)
     for i, c in enumerate(cells):
         table[i, : len(c)] = c
@@ -452,6 +472,14 @@ def generate_scene(ms: CompiledModel, blob_fnv: int, robot: CompiledModel, ns: s
     L.append(f"constexpr int GRID_NX = {nx}, GRID_NY = {ny}, CELL_K = {ck};")
     rows = ",\n    ".join("{" + ", ".join(str(int(x)) for x in r) + "}" for r in table)
     L.append(f"constexpr signed char CELL_BOX[{nx * ny}][{ck}] = {{\n    {rows}}};")
+    # opt-in free-cell goals (ackphys_env_params.goal_cells): the box-free grid cells 4-connected to
+    # the spawn cell, sorted by breadth-first distance; FREE_LE[d] = how many lie within d cells
+    _req(len(free) > 0, "a free cell next to the spawn")
+    maxd = max(d for _, _, d in free)
+    L.append(f"constexpr int NFREE = {len(free)}, FREE_MAXD = {maxd};")
+    L.append(_arr("FREE_XY", np.array([[x, y] for x, y, _ in free])))
+    L.append("constexpr int FREE_LE[" + str(maxd + 1) + "] = {" +
+             ", ".join(str(sum(1 for _, _, d in free if d <= k)) for k in range(maxd + 1)) + "};")
     # hull features of the welded meshes in the chassis frame (separating axes of box-mesh pairs)
     fns, eds = [], []
     for mh in A["meshes"]:

@@ -24,7 +24,7 @@ class AckermannRobotEnv(Env):
     def __init__(self, map_spawner=None, max_episode_steps=1000, goal_distance_threshold=0.5,
                  collision_threshold=0.15, max_linear_velocity=1.0, max_angular_velocity=1.0, render_mode=None,
                  device="cuda:0", contacts: bool = True, scene: str | None = None, action_repeat: int = 1,
-                 nohit_clear: bool = False):
+                 nohit_clear: bool = False, goal_cells: int = 0):
         super().__init__()
         # render_mode="human": the reference opens a passive MuJoCo viewer (out of scope here: no
         # window) and runs mj_forward after every mj_step (ackermann_env.py:202-207), so its
@@ -46,7 +46,8 @@ class AckermannRobotEnv(Env):
                                         max_linear_velocity=max_linear_velocity,
                                         max_angular_velocity=max_angular_velocity,
                                         poststep_obs=(render_mode == "human"), scene=scene,
-                                        action_repeat=action_repeat, nohit_clear=nohit_clear)
+                                        action_repeat=action_repeat, nohit_clear=nohit_clear,
+                                        goal_cells=goal_cells)
         # the reference's per-reset MuJoCo objects (:111-114): the batched sim owns the state
         self.model = None
         self.data = None

@@ -21,7 +21,7 @@ class AckermannVecEnv:
                  env_offset: int = 0, max_episode_steps: int = 1000, goal_distance_threshold: float = 0.5,
                  collision_threshold: float = 0.15, max_linear_velocity: float = 1.0,
                  max_angular_velocity: float = 1.0, render_mode=None, variant: str = "auto",
-                 scene: str = "flat", action_repeat: int = 1, nohit_clear: bool = False):
+                 scene: str = "flat", action_repeat: int = 1, nohit_clear: bool = False, goal_cells: int = 0):
         self.num_envs = int(num_envs)
         # the per-env constructor kwargs of the reference env (ackermann_env.py:51-60), batch-wide here
         self.max_episode_steps = max_episode_steps
@@ -39,7 +39,8 @@ class AckermannVecEnv:
                                        max_linear_velocity=max_linear_velocity,
                                        max_angular_velocity=max_angular_velocity, variant=variant,
                                        poststep_obs=(render_mode == "human"), scene=scene,
-                                       action_repeat=action_repeat, nohit_clear=nohit_clear)
+                                       action_repeat=action_repeat, nohit_clear=nohit_clear,
+                                       goal_cells=goal_cells)
         self.device = self.sim.device
         self._actions = None
         self._ep_ret = torch.zeros(self.num_envs, device=self.device)

@@ -38,7 +38,8 @@ class BatchedAckermannSim:
                  env_offset: int = 0, model_blob: bytes | None = None, max_episode_steps: int = 1000,
                  goal_distance_threshold: float = 0.5, collision_threshold: float = 0.15,
                  max_linear_velocity: float = 1.0, max_angular_velocity: float = 1.0, variant: str = "auto",
-                 poststep_obs: bool = False, scene: str = "flat", action_repeat: int = 1, nohit_clear: bool = False):
+                 poststep_obs: bool = False, scene: str = "flat", action_repeat: int = 1, nohit_clear: bool = False,
+                 goal_cells: int = 0):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("BatchedAckermannSim runs on the GPU only (no CPU fallback)")
@@ -55,10 +56,11 @@ class BatchedAckermannSim:
         self._ctx = ctx
         self.env_offset = int(env_offset)
         _lib.check(L.ackphys_set_env_offset(ctx, self.env_offset), "ackphys_set_env_offset")
-        # action_repeat / nohit_clear: opt-in task variants, NOT the reference env (include/ackphys.h)
+        # action_repeat / nohit_clear / goal_cells: opt-in task variants, NOT the reference env
+        # (include/ackphys.h; goal_cells: maze goals in free cells of the obstacle scene)
         self.params = _lib.EnvParams(int(max_episode_steps), float(goal_distance_threshold), float(collision_threshold),
                                      float(max_linear_velocity), float(max_angular_velocity), int(action_repeat),
-                                     1 if nohit_clear else 0)
+                                     1 if nohit_clear else 0, int(goal_cells))
         _lib.check(L.ackphys_set_env_params(ctx, C.byref(self.params)), "ackphys_set_env_params")
         self.variant = variant
         _lib.check(L.ackphys_set_variant(ctx, {"lane": 0, "quad": 1, "auto": 2, "lane16": 3}[variant]), "ackphys_set_variant")

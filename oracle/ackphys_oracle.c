@@ -91,6 +91,11 @@ struct or_ctx {
   /* opt-in task variants (NOT the reference; 1 / 0 = ackermann_env.py): mj_steps per env step,
      rangefinder -1 readings ignored by the collision test (include/ackphys.h) */
   int action_repeat, nohit_clear;
+  /* opt-in maze goals (goal_cells > 0, obstacle scene): the box-free cells of the box lattice
+     4-connected to the spawn cell, by breadth-first distance (free_d), centres free_xy */
+  int goal_cells, nfree;
+  double free_xy[256][2];
+  int free_d[256];
   /* resolved ids (reference looks these up by name) */
   int chassis_body, act_steer, act_rl, act_rr;
   int lidar_adr[72];
@@ -360,7 +365,7 @@ int or_create(const void* blob, size_t nbytes, or_ctx** out) {
   c->maxiter = c->m->iterations;
   c->chassis_body = c->m->jnt_bodyid[0]; /* the free joint's body ("chassis") */
   c->max_steps = 1000; c->goal_thresh = 0.5; c->coll_thresh = 0.15; c->max_lin = 1.0; c->max_ang = 1.0;
-  c->action_repeat = 1; c->nohit_clear = 0;
+  c->action_repeat = 1; c->nohit_clear = 0; c->goal_cells = 0; c->nfree = 0;
   /* BicycleController actuator lookup by name (controller.py:94-96): steering servo on the
      first limited hinge, rear drives on the first two hinges -- resolved by trnid order. */
   c->act_steer = 0; c->act_rl = 1; c->act_rr = 2;
@@ -394,6 +399,77 @@ void or_set_env_params(or_ctx* c, int max_steps, double goal, double coll, doubl
 void or_set_env_variant(or_ctx* c, int action_repeat, int nohit_clear) {
   c->action_repeat = action_repeat < 1 ? 1 : action_repeat;
   c->nohit_clear = nohit_clear != 0;
+}
+
+/* Free maze cells of the world's static boxes: the lattice origin is the boxes' lowest corner and
+   its pitch the smallest box footprint; a cell is free when no box overlaps its interior; cells
+   4-connected to the spawn's cell are listed in breadth-first order, sorted by (distance, row,
+   column), the spawn cell left out. Returns the count, 0 when the world has no boxes, -1 on a
+   lattice the tables cannot hold. */
+static int free_cells(or_ctx* c) {
+  const apm_model_t* m = c->m;
+  double x0 = 1e300, y0 = 1e300, x1 = -1e300, y1 = -1e300, cell = 1e300;
+  int nb = 0;
+  /* static (world-welded) boxes; their bodies sit at the world origin unrotated (model/codegen.py
+     checks that for the scene), so geom_pos + body_pos is the world centre */
+#define OR_STATIC_BOX(g) (m->geom_type[g] == APM_GEOM_BOX && m->body_weldid[m->geom_bodyid[g]] == 0)
+#define OR_BOX_C(g, k) (m->geom_pos[g][k] + m->body_pos[m->geom_bodyid[g]][k])
+  for (int g = 0; g < m->ngeom; g++) {
+    if (!OR_STATIC_BOX(g)) continue;
+    nb++;
+    x0 = fmin(x0, OR_BOX_C(g, 0) - m->geom_size[g][0]); x1 = fmax(x1, OR_BOX_C(g, 0) + m->geom_size[g][0]);
+    y0 = fmin(y0, OR_BOX_C(g, 1) - m->geom_size[g][1]); y1 = fmax(y1, OR_BOX_C(g, 1) + m->geom_size[g][1]);
+    cell = fmin(cell, 2 * fmin(m->geom_size[g][0], m->geom_size[g][1]));
+  }
+  if (!nb) return 0;
+  const int nx = (int)ceil((x1 - x0) / cell - 1e-9), ny = (int)ceil((y1 - y0) / cell - 1e-9);
+  if (nx * ny > 256) return -1;
+  int occ[256] = {0}, dist[256], queue[256];
+  for (int g = 0; g < m->ngeom; g++) {
+    if (!OR_STATIC_BOX(g)) continue;
+    for (int iy = 0; iy < ny; iy++)
+      for (int ix = 0; ix < nx; ix++) {
+        const double cx = x0 + ix * cell, cy = y0 + iy * cell, e = 1e-6;
+        if (OR_BOX_C(g, 0) - m->geom_size[g][0] < cx + cell - e && OR_BOX_C(g, 0) + m->geom_size[g][0] > cx + e &&
+            OR_BOX_C(g, 1) - m->geom_size[g][1] < cy + cell - e && OR_BOX_C(g, 1) + m->geom_size[g][1] > cy + e)
+          occ[iy * nx + ix] = 1;
+      }
+  }
+#undef OR_STATIC_BOX
+#undef OR_BOX_C
+  const int sx = (int)floor((m->spawn[0] - x0) / cell), sy = (int)floor((m->spawn[1] - y0) / cell);
+  if (sx < 0 || sx >= nx || sy < 0 || sy >= ny || occ[sy * nx + sx]) return -1;
+  for (int i = 0; i < nx * ny; i++) dist[i] = -1;
+  int head = 0, tail = 0;
+  dist[sy * nx + sx] = 0;
+  queue[tail++] = sy * nx + sx;
+  while (head < tail) {
+    const int q = queue[head++], qx = q % nx, qy = q / nx;
+    const int nbr[4][2] = {{qx + 1, qy}, {qx - 1, qy}, {qx, qy + 1}, {qx, qy - 1}};
+    for (int k = 0; k < 4; k++) {
+      const int ax = nbr[k][0], ay = nbr[k][1];
+      if (ax < 0 || ax >= nx || ay < 0 || ay >= ny || occ[ay * nx + ax] || dist[ay * nx + ax] >= 0) continue;
+      dist[ay * nx + ax] = dist[q] + 1;
+      queue[tail++] = ay * nx + ax;
+    }
+  }
+  int n = 0;
+  for (int d = 1; d <= nx * ny; d++)  /* by distance, then row-major (row, column) */
+    for (int i = 0; i < nx * ny; i++)
+      if (dist[i] == d) {
+        c->free_xy[n][0] = x0 + (i % nx + 0.5) * cell;
+        c->free_xy[n][1] = y0 + (i / nx + 0.5) * cell;
+        c->free_d[n++] = d;
+      }
+  return n;
+}
+int or_set_goal_cells(or_ctx* c, int goal_cells) {
+  if (goal_cells <= 0) { c->goal_cells = 0; return 0; }
+  const int n = free_cells(c);
+  if (n <= 0) { set_err("goal_cells needs a world of static boxes with a free spawn cell"); return -1; }
+  c->nfree = n;
+  c->goal_cells = goal_cells;
+  return 0;
 }
 
 /* ------------------------------------------------------------------ mj_kinematics */
@@ -1731,6 +1807,13 @@ static void env_reset(const or_ctx* c, or_data* d, double* st, int env, uint64_t
      measures from the reset pose), whatever the spawn point */
   st[ST_GOAL] = dd * cos(th);
   st[ST_GOAL + 1] = dd * sin(th);
+  if (c->goal_cells > 0) { /* opt-in maze task: free cell floor(u * #cells within goal_cells) */
+    uint32_t nle = 0;
+    for (int i = 0; i < c->nfree; i++) nle += c->free_d[i] <= c->goal_cells;
+    const uint32_t i = (uint32_t)(((uint64_t)(ctr[0] >> 8) * nle) >> 24);
+    st[ST_GOAL] = c->free_xy[i][0] - m->spawn[0];
+    st[ST_GOAL + 1] = c->free_xy[i][1] - m->spawn[1];
+  }
   memcpy(st + ST_REF, d->xpos[c->chassis_body], sizeof(double) * 3);
   st[ST_STEP] = 0;
   st[ST_EPIS] = episode;

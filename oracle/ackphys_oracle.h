@@ -25,6 +25,10 @@ void or_set_env_params(or_ctx* ctx, int max_episode_steps, double goal_distance_
 /* opt-in task variant (not the reference): action_repeat mj_steps per env step; nohit_clear != 0
  * ignores -1 (no-hit) rangefinder readings in the collision test (include/ackphys.h) */
 void or_set_env_variant(or_ctx* ctx, int action_repeat, int nohit_clear);
+/* opt-in maze goals (not the reference): goal_cells > 0 draws reset goals at the centres of the free
+ * box-lattice cells within goal_cells breadth-first cells of the spawn (include/ackphys.h);
+ * -1 if the world has no such lattice */
+int or_set_goal_cells(or_ctx* ctx, int goal_cells);
 
 /* ackphys_step on host buffers (flags: ACKPHYS_CONTACTS | ACKPHYS_AUTORESET | ACKPHYS_POSTSTEP_OBS).
  * terminal_obs, info, episode may be NULL. nthreads <= 0: OpenMP default. */

@@ -53,6 +53,7 @@ def lib():
         L.or_controller2.argtypes = [P, C.c_double, C.c_double, P]
         L.or_set_env_params.argtypes = [P, i32, C.c_double, C.c_double, C.c_double, C.c_double]
         L.or_set_env_variant.argtypes = [P, i32, i32]
+        L.or_set_goal_cells.argtypes = [P, i32]
         L.or_philox.argtypes = [P, P, P]
         L.or_model_struct_size.restype = i32
         L.or_observe_raw.argtypes = [P, P, P, P, P, P, P, P, P, P]
@@ -88,10 +89,13 @@ class Oracle:
         lib().or_set_solver(self._ctx, tolerance, maxiter)
 
     def set_env_params(self, max_episode_steps=1000, goal_distance_threshold=0.5, collision_threshold=0.15,
-                       max_linear_velocity=1.0, max_angular_velocity=1.0, action_repeat=1, nohit_clear=False):
+                       max_linear_velocity=1.0, max_angular_velocity=1.0, action_repeat=1, nohit_clear=False,
+                       goal_cells=0):
         lib().or_set_env_params(self._ctx, max_episode_steps, goal_distance_threshold, collision_threshold,
                                 max_linear_velocity, max_angular_velocity)
         lib().or_set_env_variant(self._ctx, int(action_repeat), int(bool(nohit_clear)))
+        if lib().or_set_goal_cells(self._ctx, int(goal_cells)) != 0:
+            raise ValueError("goal_cells needs the obstacle scene (a world of static boxes)")
 
     def set_env_offset(self, off: int):
         lib().or_set_env_offset(self._ctx, off)

@@ -237,3 +237,37 @@ def test_variant_refusals():
         b.step(torch.zeros(16, 2, device=DEV))
     with pytest.raises((RuntimeError, ValueError)):
         _sim(16, action_repeat=0)
+    with pytest.raises(RuntimeError):
+        _sim(16, goal_cells=3)  # free-cell goals need the obstacle scene's maze
+    with pytest.raises((RuntimeError, ValueError)):
+        _sim(16, scene="obstacles", goal_cells=-1)
+
+
+@pytest.mark.parametrize("goal_cells", [1, 3, 10])
+def test_maze_goals_match_oracle(goal_cells):
+    """Opt-in free-cell goals (goal_cells > 0, obstacle scene): the kernels' reset goals and the
+    goals of auto-resets inside steps (on the quad mapping's reset path) equal the oracle's
+    (tests/test_maze_goals.py pins the oracle's cells to the kernels' table)."""
+    from mujoco_playground_amd import _lib
+    from mujoco_playground_amd.sim import ST_GOAL, ST_EPIS
+    n = 301
+    kw = dict(seed=21, contacts=True, scene="obstacles", max_episode_steps=3, goal_cells=goal_cells)
+    a = _sim(n, **kw)
+    a.reset()
+    o = _oracle(_lib.load_blob("obstacles"), max_episode_steps=3, goal_cells=goal_cells)
+    st = np.zeros((n, 44))
+    o.reset(st, seed=21)
+    torch.cuda.synchronize()
+    g = a.state[ST_GOAL:ST_GOAL + 2].double().cpu().numpy().T
+    np.testing.assert_allclose(g, st[:, ST_GOAL:ST_GOAL + 2], atol=2e-6)
+    acts = a.random_actions(7, seed=4)
+    for k in range(7):  # two truncations at 3 steps: new episodes, new goals
+        a.step(acts[k])
+    torch.cuda.synchronize()
+    ep = f64_state(a.state)[:, ST_EPIS]
+    assert ep.min() >= 3
+    st2 = np.zeros((n, 44))
+    st2[:, ST_EPIS] = ep - 1  # the oracle's reset draws the goal of episode ep
+    o.reset(st2, seed=21)
+    g = a.state[ST_GOAL:ST_GOAL + 2].double().cpu().numpy().T
+    np.testing.assert_allclose(g, st2[:, ST_GOAL:ST_GOAL + 2], atol=2e-6)

@@ -2,7 +2,7 @@
 learning curve + deterministic goal-reach evaluation -> one JSON line per evaluation.
 
     python tools/train_ppo.py [--envs 4096] [--iters 400] [--eval-every 25] [--out gpurun_out/train_ppo.jsonl]
-                              [--action-repeat R] [--nohit-clear] [--scene flat|obstacles]
+                              [--action-repeat R] [--nohit-clear] [--scene flat|obstacles] [--goal-cells D]
 
 Env: make_ackermann_env(env_type="vec") defaults (the reference's make_env signature:
 max_linear_velocity 0.5, goal_distance_threshold 0.3), contacts on. PPO: SB3 semantics
@@ -11,7 +11,9 @@ max_linear_velocity 0.5, goal_distance_threshold 0.3), contacts on. PPO: SB3 sem
 The reference task itself is not learnable as configured (2 s episodes at <= 0.5 m/s against 2-8 m
 goals, and a -50 "collision" on every step any lidar ray misses). --action-repeat R (R mj_steps per
 env step) and --nohit-clear (a missed ray is no obstacle) are the opt-in variant of
-include/ackphys.h that makes it learnable; both default to the reference.
+include/ackphys.h that makes it learnable; both default to the reference. In the obstacle scene the
+reference's goals mostly lie behind walls; --goal-cells D (opt-in) draws them at free maze cells
+within D breadth-first cells of the spawn.
 """
 import argparse
 import json
@@ -46,6 +48,14 @@ def evaluate(model, n=1024, horizon=1000, seed=123, **env_kw):
         if t % 50 == 49 and bool(done.all()):
             break
     succ = float(done.float().mean())
+    # success per distinct goal (maze goals: one entry per free cell; reference goals: too many, skipped)
+    goals = torch.round(sim.state[37:39].t() * 100).long()
+    per_goal = None
+    uniq, inv = torch.unique(goals, dim=0, return_inverse=True)
+    if uniq.shape[0] <= 32:
+        per_goal = {f"{int(g[0]) / 100:+.2f},{int(g[1]) / 100:+.2f}": round(float(done[inv == i].float().mean()), 3)
+                    for i, g in enumerate(uniq)}
+    evaluate.per_goal = per_goal
     return succ, (float(t_goal[done].mean()) if bool(done.any()) else None), float(ret.mean())
 
 
@@ -66,6 +76,7 @@ def main():
     ap.add_argument("--action-repeat", type=int, default=1, help="1 = the reference (opt-in variant)")
     ap.add_argument("--nohit-clear", action="store_true", help="off = the reference (opt-in variant)")
     ap.add_argument("--scene", default="flat", choices=["flat", "obstacles"])
+    ap.add_argument("--goal-cells", type=int, default=0, help="0 = the reference's goals (opt-in maze variant)")
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--epochs", type=int, default=10)
@@ -73,7 +84,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     env_kw = dict(collision_threshold=a.collision_threshold, action_repeat=a.action_repeat,
-                  nohit_clear=a.nohit_clear, scene=a.scene)
+                  nohit_clear=a.nohit_clear, scene=a.scene, goal_cells=a.goal_cells)
     horizon = a.max_episode_steps
     venv = make_ackermann_env(env_type="vec", num_envs=a.envs, device=dev, seed=a.seed,
                               max_episode_steps=a.max_episode_steps, **env_kw)
@@ -101,7 +112,7 @@ def main():
                    "ep_rew_mean": lg.get("rollout/ep_rew_mean"), "episodes": lg.get("rollout/episodes_total"),
                    "value_loss": lg.get("train/value_loss"), "approx_kl": lg.get("train/approx_kl"),
                    "std": lg.get("train/std"), "eval_success": succ, "eval_steps_to_goal": tg,
-                   "eval_return": ret}
+                   "eval_return": ret, "eval_success_per_goal": evaluate.per_goal}
             print(json.dumps(rec), flush=True)
             out.write(json.dumps(rec) + "\n")
             out.flush()
