@@ -892,15 +892,30 @@ extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce1_kernel(const f
   __shared__ float lred[256];
   const int tid = threadIdx.x, pl = tid & (R1_P - 1), g = tid / R1_P;
   const int pidx = blockIdx.x * R1_P + pl;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (pidx < P) {
-    int b = g;
-    for (; b + 3 * R1_G < nblk; b += 4 * R1_G) {
+  // all R1_K of this thread's rows in flight at once (one memory latency, not four), then summed in
+  // the order of the original loop -- blocks of 4 rows into acc[0..3] while a whole block of 4
+  // remains, the tail rows into acc[0] -- so the result is the same, bit for bit
+  constexpr int R1_K = GRAD_MAX_BLOCKS / R1_G;
+  static_assert(R1_K % 4 == 0, "row blocks of four");
+  float x[R1_K];
 #pragma unroll
-      for (int i = 0; i < 4; i++) acc[i] += gpart[(size_t)(b + i * R1_G) * P + pidx];
-    }
-    for (; b < nblk; b += R1_G) acc[0] += gpart[(size_t)b * P + pidx];
+  for (int k = 0; k < R1_K; k++) {
+    const int b = g + k * R1_G;
+    x[k] = (pidx < P && b < nblk) ? gpart[(size_t)b * P + pidx] : 0.0f;
   }
+  int nmain = 0;  // blocks j with g + 4 R1_G j + 3 R1_G < nblk (a prefix)
+#pragma unroll
+  for (int j = 0; j < R1_K / 4; j++) nmain += (g + 4 * R1_G * j + 3 * R1_G < nblk) ? 1 : 0;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < R1_K / 4; j++)
+    if (j < nmain) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
+    }
+#pragma unroll
+  for (int k = 0; k < R1_K; k++)
+    if (k >= 4 * nmain) acc[0] += x[k];  // rows past nblk are 0.0f: adding them changes nothing
   red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (tid < R1_P && pidx < P) {
@@ -977,22 +992,25 @@ extern "C" __global__ void __launch_bounds__(ADAM_THREADS) ackppo_adam_kernel(fl
                                                                               float max_norm, float b1, float b2,
                                                                               float eps, float step_size,
                                                                               float bc2_sqrt, float* norm_out) {
-  __shared__ float red[ADAM_THREADS];
+  constexpr int NW = ADAM_THREADS / 64;
+  __shared__ float red[NW];
   const int tid = threadIdx.x;
-  // every block forms the global norm itself (75 KB from L2) instead of a second launch
+  // every block forms the global norm itself (75 KB from L2) instead of a second launch: per-thread
+  // sums, a shuffle tree per wave, then the NW wave sums in a fixed order from LDS behind one
+  // barrier (a 1024-wide LDS tree took 10 barriers)
   float ss = 0.0f;
 #pragma unroll 8
   for (int i = tid; i < P; i += ADAM_THREADS) {
     const float gi = grad[i] * scale;
     ss = fmaf(gi, gi, ss);
   }
-  red[tid] = ss;
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
-  for (int o = ADAM_THREADS / 2; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
-    __syncthreads();
-  }
-  const float norm = sqrtf(red[0]);
+  float tot = 0.0f;
+#pragma unroll
+  for (int w = 0; w < NW; w++) tot += red[w];
+  const float norm = sqrtf(tot);
   const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
   if (blockIdx.x == 0 && tid == 0 && norm_out) norm_out[0] = norm;
   const int i = blockIdx.x * ADAM_THREADS + tid;
@@ -1216,7 +1234,8 @@ int reduce_launch(float* grad_partial, const float* loss_partial, int nblk, floa
 
 int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, void* stream) {
-  if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0) return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments");
+  if (!grad_partial || !loss_partial || !grad || !loss || nblk <= 0 || nblk > GRAD_MAX_BLOCKS)
+    return fail(ACKPPO_EINVAL, "ackppo_reduce: bad arguments (nblk: 1..ackppo_grad_blocks(batch))");
   return reduce_launch(grad_partial, loss_partial, nblk, ent_coef, grad, loss, 0, stream);
 }
 
