@@ -93,8 +93,9 @@ typedef struct ackphys_env_params {
 } ackphys_env_params;
 int ackphys_set_env_params(ackphys_t* ctx, const ackphys_env_params* params);
 
-/* Step-kernel mapping: ACKPHYS_VARIANT_QUAD runs each env on 4 lanes of a wavefront (one per
- * wheel: contacts, Jacobian rows, Hessian/line-search partials, a quarter of the rays);
+/* Step-kernel mapping: ACKPHYS_VARIANT_QUAD runs each env's dynamics on 8 lanes of a wavefront
+ * (two per wheel, each with half of the wheel's contact slots: Jacobian rows, Hessian/line-search
+ * partials; the observation on 4 lanes, a quarter of the rays each; 8 envs per wave);
  * ACKPHYS_VARIANT_LANE runs each env on one lane; ACKPHYS_VARIANT_AUTO (default) picks QUAD when
  * contacts are enabled and LANE otherwise. Same results up to f32 summation order. */
 #define ACKPHYS_VARIANT_LANE 0
