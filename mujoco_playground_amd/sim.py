@@ -93,6 +93,12 @@ class BatchedAckermannSim:
     def _stream(self):
         return C.c_void_p(_raw_stream(self._dev_index))
 
+    def set_goal_cells(self, goal_cells: int):
+        """Opt-in maze goals (obstacle scene): change goal_cells between launches; it applies to the
+        goals of later resets (e.g. a curriculum over the maze)."""
+        self.params.goal_cells = int(goal_cells)
+        _lib.check(_lib.lib().ackphys_set_env_params(self._ctx, C.byref(self.params)), "ackphys_set_env_params")
+
     def reset(self, mask: torch.Tensor | None = None, seed: int | None = None) -> torch.Tensor:
         if seed is not None:
             self.seed = int(seed)

@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--nohit-clear", action="store_true", help="off = the reference (opt-in variant)")
     ap.add_argument("--scene", default="flat", choices=["flat", "obstacles"])
     ap.add_argument("--goal-cells", type=int, default=0, help="0 = the reference's goals (opt-in maze variant)")
+    ap.add_argument("--goal-cells-start", type=int, default=0,
+                    help="> 0: curriculum, goal_cells grows from this value by one every --goal-cells-every iterations")
+    ap.add_argument("--goal-cells-every", type=int, default=200)
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--epochs", type=int, default=10)
@@ -101,18 +104,24 @@ def main():
            "eval_return": ret}
     print(json.dumps(rec), flush=True)
     out.write(json.dumps(rec) + "\n")
+    def cells_at(it):
+        if a.goal_cells_start <= 0 or a.goal_cells <= 0:
+            return a.goal_cells
+        return min(a.goal_cells, a.goal_cells_start + it // a.goal_cells_every)
     for it in range(1, a.iters + 1):
+        if cells_at(it) != cells_at(it - 1) or it == 1:
+            venv.sim.set_goal_cells(cells_at(it))
         model.learn(total_timesteps=model.n_steps * a.envs)  # one rollout + update per call
         if it % a.eval_every == 0 or it == a.iters:
             torch.cuda.synchronize()
             wall = time.perf_counter() - t0
-            succ, tg, ret = evaluate(model, horizon=horizon, **env_kw)
+            succ, tg, ret = evaluate(model, horizon=horizon, **dict(env_kw, goal_cells=a.goal_cells))
             lg = model.logger
             rec = {"iter": it, "env_steps": it * model.n_steps * a.envs, "wall_s": round(wall, 2),
                    "ep_rew_mean": lg.get("rollout/ep_rew_mean"), "episodes": lg.get("rollout/episodes_total"),
                    "value_loss": lg.get("train/value_loss"), "approx_kl": lg.get("train/approx_kl"),
                    "std": lg.get("train/std"), "eval_success": succ, "eval_steps_to_goal": tg,
-                   "eval_return": ret, "eval_success_per_goal": evaluate.per_goal}
+                   "eval_return": ret, "eval_success_per_goal": evaluate.per_goal, "goal_cells_train": cells_at(it)}
             print(json.dumps(rec), flush=True)
             out.write(json.dumps(rec) + "\n")
             out.flush()
