@@ -52,11 +52,14 @@ SETTLE_STEPS = 200
 
 
 def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant="auto", scene="flat", graph=False,
-            per_step=False):
+            per_step=False, buffers=False):
     """Times `steps` random-ctrl steps of the env shard. Default: ONE ackphys_rollout launch runs the
     K pre-drawn action rows (every step computed and its outputs written, exactly K ackphys_step
-    calls' results -- tests/test_gpu_rollout.py); per_step=True: K ackphys_step launches (the call
-    pattern of a policy-in-the-loop RL step), graph=True: those K launches replayed from a hipGraph."""
+    calls' results -- tests/test_gpu_rollout.py), each step's outputs overwriting the last in place;
+    buffers=True: the same launch writing every step's obs / reward / flags into its own slice of a
+    [K, ...] rollout buffer (per_step_outputs=1: the bytes a consumer of every step's observation
+    needs leave the chip); per_step=True: K ackphys_step launches (the call pattern of a
+    policy-in-the-loop RL step), graph=True: those K launches replayed from a hipGraph."""
     sim = BatchedAckermannSim(n_env, device, seed=seed, contacts=contacts,
                               env_offset=shard.env_offset(rank, n_env), variant=variant, scene=scene)
     sim.reset()
@@ -80,7 +83,8 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
         sim.state.copy_(snap[0])  # capture launches nothing, but restore anyway
         sim.episode.copy_(snap[1])
     stream = torch.cuda.current_stream(device)
-    launch = None if (per_step or g is not None) else sim.rollout_launcher(timed_actions)
+    launch = None if (per_step or g is not None) else sim.rollout_launcher(
+        timed_actions, outputs=sim.rollout_buffers(steps) if buffers else None)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
     shard.barrier(world, device)
@@ -149,10 +153,33 @@ def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_
     train_ms = sum(e[2 * i + 1].elapsed_time(e[2 * i + 2]) for i in range(iters)) / iters
     steps = iters * n_steps * n_env * world
     nmb = (n_steps * n_env + batch_size - 1) // batch_size
+    dp_path = None
+    if world == 1:
+        # the world > 1 update path on one GPU: ackppo_train's data-parallel sequence (advantage
+        # moments + 2 f64 all-reduces per epoch, one 75 KB f32 all-reduce per minibatch) over a one-rank
+        # native RCCL communicator, timed on the same rollout buffer (untimed first call)
+        model.set_collective("rccl")
+        model.train()
+        ed = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize(device)
+        ed[0].record(stream)
+        for _ in range(iters):
+            model.train()
+        ed[1].record(stream)
+        torch.cuda.synchronize(device)
+        dp_ms = ed[0].elapsed_time(ed[1]) / iters
+        model.set_collective(None)
+        dp_path = {"update_ms": dp_ms, "update_us_per_minibatch": dp_ms * 1e3 / (nmb * n_epochs),
+                   "ratio_to_single_rank_update": dp_ms / train_ms,
+                   "collectives_per_iteration": n_epochs * (nmb + 2),
+                   "bytes_per_minibatch_allreduce": 4 * 18764,
+                   "note": "ackppo_train with the native RCCL hook (ackppo_rccl_allreduce) on a one-rank "
+                           "communicator: the data-parallel sequence every rank of configs[3] runs, each "
+                           "collective enqueued from C (no per-minibatch host round trip)"}
     return {"value": steps / el, "unit": "env-steps/s (rollout + update, all ranks)",
             "rollout_env_steps_per_s": n_steps * n_env * world / (roll_ms * 1e-3),
             "rollout_ms": roll_ms, "update_ms": train_ms, "minibatch_updates_per_iter": nmb * n_epochs,
-            "update_us_per_minibatch": train_ms * 1e3 / (nmb * n_epochs),
+            "update_us_per_minibatch": train_ms * 1e3 / (nmb * n_epochs), "dp_update_path": dp_path,
             "rollout_path": ("one ackphys_ppo_rollout launch per rollout (policy + env steps + bootstrap fused)"
                              if model.fused_rollout else "ackppo_act + ackphys_step launches per step"),
             "config": f"{scene} scene, {n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} "
@@ -280,14 +307,14 @@ def _profile(name: str):
         return None
 
 
-def load_pmc(kern_name: str, contacts: bool, steps: int):
+def load_pmc(kern_name: str, contacts: bool, steps: int, buffers: bool = False):
     """PMC summary of the kernel from the committed rocprofv3 passes (tools/profile_pmc.py ->
     profiles/pmc_latest.json), for the launch length K nearest to `steps` (a launch's first-step
     loads and last-step stores are spread over its K steps); None if absent. The counters are NOT
     measured in this run: the returned entry names its source."""
     d = _profile("pmc_latest.json") or {}
     cands = [v for v in d.values() if isinstance(v, dict) and v.get("kernel") == kern_name
-             and bool(v.get("contacts")) == contacts]
+             and bool(v.get("contacts")) == contacts and bool(v.get("per_step_outputs")) == buffers]
     if not cands:
         return None
     best = min(cands, key=lambda v: abs(v["launch_steps"] - steps))
@@ -296,6 +323,7 @@ def load_pmc(kern_name: str, contacts: bool, steps: int):
 
 
 CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md constants table)
+STAMP_OVERHEAD = 0.11  # cycles the diagnostic build's LDS stamps add to the dynamics wave
 
 
 def critical_path(kern_name: str, kern_ms: float):
@@ -306,8 +334,12 @@ def critical_path(kern_name: str, kern_ms: float):
     if e is None:
         return None
     kc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
+    ratio = e["dyn_wave_cycles_per_step_median"] / kc
     return {"dyn_wave_cycles_per_step": e["dyn_wave_cycles_per_step_median"], "kernel_cycles_per_step": kc,
-            "frac_of_kernel_time": e["dyn_wave_cycles_per_step_median"] / kc, "clock_ghz_assumed": CLOCK_GHZ,
+            "diag_over_kernel_cycles": ratio, "stamp_overhead": STAMP_OVERHEAD,
+            "frac_of_kernel_time": min(1.0, ratio / (1.0 + STAMP_OVERHEAD)), "clock_ghz_assumed": CLOCK_GHZ,
+            "note": "stamped diagnostic build (its stamps add ~11 %, removed in frac_of_kernel_time, which is "
+                    "clamped at 1) against this run's kernel time at the assumed peak clock",
             "phases_median": e.get("phases_median"),
             "source": f"profiles/critical_path_latest.json ({d.get('_round', '?')}): {e.get('measured', '')}"}
 
@@ -402,6 +434,10 @@ def main():
                     help="time K ackphys_step launches instead of one ackphys_rollout launch of K steps")
     ap.add_argument("--no-per-step", action="store_true",
                     help="skip the per-step-launch legs (K ackphys_step launches of the same workloads)")
+    ap.add_argument("--no-buffer-leg", action="store_true",
+                    help="skip the rollout-buffer leg (the headline launch with per-step output slices)")
+    ap.add_argument("--buffers", action="store_true",
+                    help="time the headline launch with per-step output slices (tools/profile_pmc.py --buffers)")
     ap.add_argument("--check-launch", action="store_true",
                     help="ranks check the world and backend, print one JSON line and exit (no GPU work)")
     a = ap.parse_args()
@@ -437,7 +473,8 @@ def main():
     # a throwaway sim first, whatever ran before (so the value does not depend on --no-secondary)
     clock_warm(device, a.envs)
     sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
-                                             variant=a.variant, graph=a.graph, per_step=a.per_step)
+                                             variant=a.variant, graph=a.graph, per_step=a.per_step,
+                                             buffers=a.buffers)
     value = total_envs * a.steps / elapsed
 
     def per_step_leg(c, scene="flat"):
@@ -448,6 +485,24 @@ def main():
                 "note": "K ackphys_step launches (one per step) instead of one ackphys_rollout launch"}
     do_per_step = fused and not a.no_per_step
     per_step_launch = per_step_leg(contacts) if do_per_step else None
+
+    def buffer_leg(c):
+        """the headline launch with per-step output slices (a [K][79][N] obs + reward / flag rollout
+        buffer): every step's 690 algorithmic bytes per env really leave the chip"""
+        _, el, km, _, _ = run_gpu(a.envs, a.steps, a.warmup, c, rank, world, device, variant=a.variant, buffers=True)
+        ach = bpe * a.envs / (km * 1e-3) / 1e9
+        pm = load_pmc(kern, c, a.steps, buffers=True)
+        return {"value": total_envs * a.steps / el, "ms_per_step": el * 1e3 / a.steps, "kernel_ms": km,
+                "achieved_GBps": ach, "peak_GBps": HBM_PEAK_GBS, "frac": ach / HBM_PEAK_GBS,
+                "counter_bytes_per_step": pm.get("hbm_bytes_per_step") if pm else None,
+                "counter_source": pm["source"] if pm else None,
+                "note": "same kernel and workload as the headline with per_step_outputs=1: obs [K][79][N], reward "
+                        "and term/trunc [K][N] each step into its own slice (ackermann_env.py:210-229 returns the "
+                        "obs every step); achieved = the algorithmic 690 B per env-step / event-timed kernel time"}
+    bpe = algorithmic_bytes_per_env_step()
+    kern = "quad" if (a.variant == "quad" or (a.variant == "auto" and contacts)) else ("" if contacts else "nc")
+    kern = ("ackphys_rollout" if fused else "ackphys_step") + (f"_{kern}" if kern else "") + "_kernel"
+    rollout_buffer = buffer_leg(contacts) if (fused and not a.no_buffer_leg) else None
     secondary = None
     if sec_run is not None:
         _, el2, km2, _, _ = sec_run
@@ -472,10 +527,7 @@ def main():
     parity = base = None
     if rank == 0 and not a.no_cpu:
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
-    bpe = algorithmic_bytes_per_env_step()
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
-    kern = "quad" if (a.variant == "quad" or (a.variant == "auto" and contacts)) else ("" if contacts else "nc")
-    kern = ("ackphys_rollout" if fused else "ackphys_step") + (f"_{kern}" if kern else "") + "_kernel"
     pmc = load_pmc(kern, contacts, a.steps)
     valu = None
     if pmc and pmc.get("valu_insts_per_wave_step"):
@@ -507,8 +559,11 @@ def main():
                        "backend": backend,
                        "launcher": ("bench.py --gpus N (torch.distributed.run children)" if os.environ.get(
                            "ACKPHYS_SPAWNED") else ("torchrun" if world > 1 else "single process"))},
-            "roofline": {"bound": "valu-latency", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
+                         "limiter": "valu-latency",
+                         "frac_basis": ("the headline launch (per-step outputs overwritten in place); the rollout_buffer "
+                                        "leg gives the same figure with every step's outputs written to its own slice"),
                          "traffic": (pmc["hbm_bytes_per_step"] * a.steps if (pmc and fused) else
                                      (pmc["hbm_bytes_per_step"] if pmc else None)),
                          "traffic_unit": "HBM bytes per launch (PMC, profiled separately: see hbm.counter_source)",
@@ -522,16 +577,16 @@ def main():
                                           "nominal bytes); " + (f"one launch runs all {a.steps} timed steps, so per "
                                                                 "launch bytes and time both scale by the step count"
                                                                 if fused else "one launch per step")),
-                         "note": ("bound = the dynamics wave's dependent f32 VALU chain (critical_path: its cycles "
-                                  "per step are the kernel's); 4096 envs = 64 dynamics + 64 observation + 64 prep "
-                                  "waves (lane mapping, contacts off), 192 of 1024 SIMDs. achieved/peak/frac are "
-                                  "the HBM figures the contract asks for, nominal bytes over kernel time: HBM is "
-                                  "not what limits this kernel")},
+                         "note": ("bound/achieved/peak/frac: the HBM roofline the contract asks for, algorithmic "
+                                  "bytes over kernel time. HBM is not what limits this kernel: limiter = the "
+                                  "dynamics wave's dependent f32 VALU chain (critical_path: its cycles per step "
+                                  "are the kernel's); 4096 envs = 64 dynamics + 64 observation + 64 prep waves "
+                                  "(lane mapping, contacts off), 192 of 1024 SIMDs")},
             "timing": ("one ackphys_rollout launch of the K timed steps (pre-drawn actions resident in HBM; every "
                        "step computed and its outputs written)" if fused else
                        ("K ackphys_step launches replayed from a hipGraph" if a.graph else
                         "K ackphys_step launches")),
-            "per_step_launch": per_step_launch,
+            "per_step_launch": per_step_launch, "rollout_buffer": rollout_buffer,
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
             "obstacles": obstacles,
         }

@@ -151,14 +151,79 @@ int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg
  * grad_scale 1 and t = adam_step0 + m + 1 (step_size = learning_rate / (1 - beta1^t), bc2_sqrt =
  * sqrt(1 - beta2^t), float64 as torch computes them). The same kernels and arithmetic as the
  * per-minibatch calls (SB3 PPO.train, on_policy_algorithm / ppo.py:196-279 of SB3 2.7.0); the
- * loop runs on the host in C so the launches queue back to back. Data-parallel learners
- * (world > 1) call grad / reduce / all-reduce / adam per minibatch instead. */
+ * loop runs on the host in C so the launches queue back to back. ackppo_train (below) runs
+ * whole training phases, single-rank or data-parallel, the same way. */
 int ackppo_epoch(float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
                  const float* advantages, const float* returns, const int32_t* idx, int n_idx, int batch,
                  const float* stats, float clip_range, float ent_coef, float vf_coef, float max_grad_norm,
                  double learning_rate, double beta1, double beta2, float eps, int64_t adam_step0,
                  float* grad_partial, float* loss_partial, float* grad, float* loss_acc, float* exp_avg,
                  float* exp_avg_sq, float* grad_norm_out, void* stream);
+
+/* ---- the whole PPO.train() in one host call, single rank or data-parallel ----
+ *
+ * Collective hook: SUM all-reduce, in place, of `count` elements of `dtype` (ACKPPO_F32 / ACKPPO_F64)
+ * at device pointer `buf`, ordered on `stream` after the work already enqueued there; 0 = success.
+ * ackppo_rccl_allreduce (below) is one, over a native RCCL communicator; a caller may pass its own
+ * (e.g. a host-staged gloo rehearsal). NULL with world == 1: no collective. */
+#define ACKPPO_F32 0
+#define ACKPPO_F64 1
+typedef int (*ackppo_allreduce_fn)(void* buf, int64_t count, int dtype, void* user, void* stream);
+
+typedef struct {
+  /* rollout buffer (this rank's shard, [T*N] samples, include order as above) */
+  const float* obs_rows;
+  const float* actions;
+  const float* old_log_prob;
+  const float* advantages;
+  const float* returns;
+  int n_idx;                /* T * N */
+  int batch;                /* per-rank minibatch (a world minibatch is world x batch samples) */
+  int n_epochs;
+  uint64_t perm_key;        /* ackppo_permutation key (seed, rank) */
+  uint32_t perm_epoch0;     /* epoch counter of the first epoch (advanced by n_epochs) */
+  int normalize_advantage;
+  float clip_range, ent_coef, vf_coef, max_grad_norm;
+  double learning_rate, beta1, beta2;
+  float eps;
+  int64_t adam_step0;       /* Adam steps taken before this call (advanced by n_epochs x nmb) */
+  /* state and scratch (device) */
+  float* params;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int32_t* perm;            /* [n_idx] */
+  float* stats;             /* [nmb][2] */
+  double* moments;          /* [3][nmb] (world > 1) */
+  float* grad_partial;      /* [ackppo_grad_blocks(batch)][NPARAM], pad words zero */
+  float* loss_partial;      /* [ackppo_grad_blocks(batch)][8] */
+  float* grad;              /* [NPARAM] */
+  float* loss_acc;          /* [8]: zeroed, then the loss columns of every minibatch added */
+  float* grad_norm_out;     /* [1] nullable: pre-clip norm of the last minibatch */
+  /* data parallelism */
+  int world;
+  ackppo_allreduce_fn allreduce;
+  void* allreduce_user;
+} ackppo_train_desc;
+
+/* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch
+ * shuffle (ackppo_permutation), the advantage statistics of every minibatch (world 1:
+ * ackppo_adv_stats; world > 1: ackppo_adv_moments phase 0 -> all-reduce of 2 x nmb f64 -> phase 1 ->
+ * all-reduce of nmb f64 -> ackppo_adv_finalize), then per minibatch ackppo_grad -> reduce ->
+ * [all-reduce of NPARAM f32] -> ackppo_adam (grad_scale 1/world). Every launch and collective is
+ * enqueued back to back from this one call: no per-minibatch host round trip (the host never waits
+ * on the device, unless the hook itself does). World 1 without a hook: the same launches as
+ * ackppo_epoch per epoch, bit for bit. A hook at world 1 runs the data-parallel sequence over one
+ * rank (the same results: the moments give ackppo_adv_stats' statistics bit for bit). */
+int ackppo_train(const ackppo_train_desc* d, void* stream);
+
+/* Native RCCL communicator for the trainer's collectives (one process per GPU; the library is
+ * the process's RCCL -- the one torch loaded if any, else librccl.so.1 -- opened at run time).
+ * Rank 0 makes the 128-byte unique id, the caller distributes it (e.g. a torch.distributed
+ * broadcast), every rank calls ackppo_rccl_init on its current device. */
+int ackppo_rccl_unique_id(void* id128);
+int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm);
+int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void* stream); /* an ackppo_allreduce_fn */
+int ackppo_rccl_destroy(void* comm);
 
 const char* ackppo_last_error(void);
 

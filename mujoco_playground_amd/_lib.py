@@ -64,6 +64,25 @@ class EnvParams(C.Structure):
                 ("action_repeat", C.c_int32), ("nohit_clear", C.c_int32), ("goal_cells", C.c_int32)]
 
 
+# ackppo_allreduce_fn (include/ackppo.h): SUM all-reduce in place of (buf, count, dtype, user, stream)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p)
+
+
+class TrainDesc(C.Structure):
+    """ackppo_train_desc (include/ackppo.h): one PPO.train() call."""
+    _fields_ = [("obs_rows", C.c_void_p), ("actions", C.c_void_p), ("old_log_prob", C.c_void_p),
+                ("advantages", C.c_void_p), ("returns", C.c_void_p), ("n_idx", C.c_int), ("batch", C.c_int),
+                ("n_epochs", C.c_int), ("perm_key", C.c_uint64), ("perm_epoch0", C.c_uint32),
+                ("normalize_advantage", C.c_int), ("clip_range", C.c_float), ("ent_coef", C.c_float),
+                ("vf_coef", C.c_float), ("max_grad_norm", C.c_float), ("learning_rate", C.c_double),
+                ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_float), ("adam_step0", C.c_int64),
+                ("params", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p), ("perm", C.c_void_p),
+                ("stats", C.c_void_p), ("moments", C.c_void_p), ("grad_partial", C.c_void_p),
+                ("loss_partial", C.c_void_p), ("grad", C.c_void_p), ("loss_acc", C.c_void_p),
+                ("grad_norm_out", C.c_void_p), ("world", C.c_int), ("allreduce", C.c_void_p),
+                ("allreduce_user", C.c_void_p)]
+
+
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, *HIPCC_FLAGS, *extra, "-o", out + ".tmp", sources[0]]
@@ -94,7 +113,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     step, include/ackphys.h) and libackppo.so (PPO learner, include/ackppo.h)."""
     # both libraries with the same flags: the policy arithmetic they share (csrc/ackppo_math.inc)
     # then compiles alike, and the fused rollout's actions equal ackppo_act's bit for bit
-    _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force, tuple(PHYS_FLAGS))
+    # libackppo opens the process's librccl.so.1 at run time (dlopen) for the trainer's collectives
+    _hipcc(PPO_LIB_PATH, PPO_SOURCES, verbose, force, tuple(PHYS_FLAGS) + ("-ldl",))
     return _hipcc(LIB_PATH, SOURCES, verbose, force, tuple(PHYS_FLAGS))
 
 
@@ -105,7 +125,8 @@ EXPORTS = ["ackphys_create", "ackphys_destroy", "ackphys_set_env_params", "ackph
 PPO_EXPORTS = ["ackppo_act", "ackppo_act_boot", "ackppo_value", "ackppo_bootstrap", "ackppo_gae", "ackppo_adv_stats",
                "ackppo_adv_moments", "ackppo_adv_finalize", "ackppo_grad",
                "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_permutation",
-               "ackppo_last_error"]
+               "ackppo_train", "ackppo_rccl_unique_id", "ackppo_rccl_init", "ackppo_rccl_allreduce",
+               "ackppo_rccl_destroy", "ackppo_last_error"]
 
 _lib = None
 _ppo = None
@@ -169,6 +190,11 @@ def ppo_lib():
     L.ackppo_permutation.argtypes = [i32, u64, u32, P, P]
     L.ackppo_epoch.argtypes = ([P] * 7 + [i32, i32, P, f32, f32, f32, f32, C.c_double, C.c_double, C.c_double, f32,
                                           i64] + [P] * 8)
+    L.ackppo_train.argtypes = [C.POINTER(TrainDesc), P]
+    L.ackppo_rccl_unique_id.argtypes = [P]
+    L.ackppo_rccl_init.argtypes = [P, i32, i32, C.POINTER(P)]
+    L.ackppo_rccl_allreduce.argtypes = [P, i64, i32, P, P]
+    L.ackppo_rccl_destroy.argtypes = [P]
     L.ackppo_last_error.restype = C.c_char_p
     _ppo = L
     return L

@@ -17,8 +17,11 @@
 //    ackppo_reduce sums the rows (coalesced over parameters); ackppo_adam applies the global
 //    norm clip and the Adam step; ackppo_epoch runs a whole epoch of minibatches in one host
 //    call. No host round trip inside an update.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>
+#include <string.h>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -708,6 +711,420 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(Gr
   PSTAMP(15);
 }
 
+// ---- ackppo_grad, one net per workgroup (default, AK_PPO_GRAD1): workgroup 2 t + net takes the
+// actor (net 0) or the critic (net 1) of tile t. Its LDS (one net's weights, the tile and its
+// activations, ~78 KB) lets TWO workgroups share a CU, so one workgroup's barrier waits and memory
+// latencies hide under the other's MFMA / VALU work (the two-net workgroup of ackppo_grad_kernel
+// filled a CU's LDS alone: 4 waves per CU, one per SIMD). Wave w owns unit tile w (16 units) of its
+// net in every product, for both 16-sample halves of the tile. D1 overwrites H1 in place once the
+// W2 gradient has read H1 (two barriers), which is what brings the footprint under 80 KB.
+#ifndef AK_PPO_GRAD1
+#define AK_PPO_GRAD1 1
+#endif
+namespace g1 {
+constexpr int T = 32, LDP = 36;  // samples per tile, padded tile row (floats)
+// weights: W1T [80][64] = [k][unit], XOR-swizzled as w1t_at (64-wide rows: the 16-bank groups of
+// the four k of an MFMA read stay distinct); W2 [unit][k] swizzled as w2_at
+constexpr int W1T = 0, W2 = W1T + 80 * H, B1 = W2 + H * H, B2 = B1 + H;
+constexpr int HW = B2 + H;            // heads: actor [2][64] (critic [1][64])
+constexpr int HB = HW + 2 * H;        // actor: b[2], log_std[2] (critic: b[1])
+constexpr int WEND = HB + 4;
+constexpr int X = WEND, H1 = X + 80 * LDP, H2 = H1 + H * LDP, D2 = H2 + H * LDP;  // D1 overwrites H1
+constexpr int GA = D2 + H * LDP;      // actor: gmu [2][LDP], glog [2][LDP]; critic: gv [LDP]
+constexpr int TOTAL = GA + 4 * LDP;
+static_assert(TOTAL * 4 * 2 <= 160 * 1024, "two one-net grad workgroups must share a CU's 160 KiB LDS");
+__device__ __forceinline__ int w1t(int k, int u) { return W1T + k * H + (u ^ (16 * (k & 3)) ^ ((k >> 2) & 15)); }
+__device__ __forceinline__ int w2(int u, int k) { return W2 + w2_at(u, k); }
+constexpr int MAX_TILES = GRAD_MAX_BLOCKS;  // partial rows: one per tile, as ackppo_grad_kernel
+}  // namespace g1
+
+__device__ __forceinline__ void stage_net(const float* __restrict__ p, float* w, int net) {
+  // all global loads first (one latency), then the LDS writes: W1 (float4 rows of 79 inputs)
+  // transposed and swizzled, W2 swizzled, the short vectors
+  constexpr int N1 = H * NOBS / 4, IT1 = (N1 + GRAD_THREADS - 1) / GRAD_THREADS, IT2 = H * H / 4 / GRAD_THREADS;
+  const int tid = threadIdx.x;
+  const float* w1 = p + (net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1);
+  const float* w2 = p + (net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2);
+  float4 v[IT1], v2[IT2];
+#pragma unroll
+  for (int j = 0; j < IT1; j++) {
+    const int i = tid + j * GRAD_THREADS;
+    if (i < N1) v[j] = reinterpret_cast<const float4*>(w1)[i];
+  }
+#pragma unroll
+  for (int j = 0; j < IT2; j++) v2[j] = reinterpret_cast<const float4*>(w2)[tid + j * GRAD_THREADS];
+  __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the scatter (one memory latency)
+  // short vectors: threads 0-63 b1, b2 and the head rows; 64-67 the head biases / log_std
+  float b1 = 0.f, b2 = 0.f, hw0 = 0.f, hw1 = 0.f, hs = 0.f;
+  if (tid < H) {
+    b1 = p[(net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + tid];
+    b2 = p[(net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + tid];
+    hw0 = p[(net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W) + tid];
+    if (!net) hw1 = p[ACKPPO_OFF_ACT_W + H + tid];
+  }
+  const int sc = tid - H;  // actor: 0, 1 action_net.bias, 2, 3 log_std; critic: 0 value_net.bias
+  const bool has_sc = sc >= 0 && sc < (net ? 1 : 4);
+  if (has_sc) hs = p[net ? ACKPPO_OFF_VAL_B : (sc < 2 ? ACKPPO_OFF_ACT_B + sc : ACKPPO_OFF_LOG_STD + sc - 2)];
+#pragma unroll
+  for (int j = 0; j < IT1; j++) {
+    const int i = tid + j * GRAD_THREADS;
+    if (i < N1) {
+      const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int r = 4 * i + c, u = r / NOBS, k = r - u * NOBS;
+        w[g1::w1t(k, u)] = e[c];
+      }
+    }
+  }
+  if (tid < H) w[g1::w1t(NOBS, tid)] = 0.0f;  // k row 79: the zero pad of the 80-deep layer-1 product
+#pragma unroll
+  for (int j = 0; j < IT2; j++) {
+    const int i = 4 * (tid + j * GRAD_THREADS), u = i / H, k = i - u * H;
+    const float e[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) w[g1::w2(u, k + c)] = e[c];
+  }
+  if (tid < H) {
+    w[g1::B1 + tid] = b1;
+    w[g1::B2 + tid] = b2;
+    w[g1::HW + tid] = hw0;
+    w[g1::HW + H + tid] = hw1;
+  }
+  if (has_sc) w[g1::HB + sc] = hs;
+}
+
+__device__ __forceinline__ float row_sum_t(const float* a) {  // 32 samples of one LDS tile row
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < g1::T; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(a + i);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  return s;
+}
+__device__ __forceinline__ float row_dot_t(const float* a, const float* b) {
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < g1::T; i += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(a + i), v = *reinterpret_cast<const float4*>(b + i);
+    s = fmaf(u.x, v.x, s);
+    s = fmaf(u.y, v.y, s);
+    s = fmaf(u.z, v.z, s);
+    s = fmaf(u.w, v.w, s);
+  }
+  return s;
+}
+
+// vector gradient items of the one-net workgroup: actor i < 64 b1 (D1 rows), < 128 b2 (D2 rows),
+// < 256 action_net.weight (gmu[d] . H2 rows), 256-257 its bias, 258-259 log_std; critic i < 64 b1,
+// < 128 b2, < 192 value_net.weight (gv . H2 rows), 192 its bias
+constexpr int G1_NVA = 260, G1_NVC = 193;
+__device__ __forceinline__ float vec_item_g1(const float* tl, int net, int i) {
+  using namespace g1;
+  if (i < 64) return row_sum_t(tl + H1 + i * LDP);  // after D1 replaced H1
+  if (i < 128) return row_sum_t(tl + D2 + (i - 64) * LDP);
+  if (net == 0) {
+    if (i < 256) return row_dot_t(tl + GA + ((i - 128) >> 6) * LDP, tl + H2 + ((i - 128) & 63) * LDP);
+    return row_sum_t(tl + GA + (i < 258 ? i - 256 : 2 + i - 258) * LDP);
+  }
+  if (i < 192) return row_dot_t(tl + GA, tl + H2 + (i - 128) * LDP);
+  return row_sum_t(tl + GA);
+}
+__device__ __forceinline__ int vec_offset_g1(int net, int i) {
+  if (i < 64) return (net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + i;
+  if (i < 128) return (net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + i - 64;
+  if (net == 0) {
+    if (i < 256) return ACKPPO_OFF_ACT_W + (i - 128);
+    return i < 258 ? ACKPPO_OFF_ACT_B + i - 256 : ACKPPO_OFF_LOG_STD + i - 258;
+  }
+  return i < 192 ? ACKPPO_OFF_VAL_W + (i - 128) : ACKPPO_OFF_VAL_B;
+}
+
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kernel(GradArgs A) {
+  using namespace g1;
+  PSTAMP(0);
+  extern __shared__ float tl[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int net = blockIdx.x & 1, tile0 = blockIdx.x >> 1, tstride = gridDim.x >> 1;
+  float* w = tl;
+  const float invB = 1.0f / (float)A.batch;
+  const int ntiles = (A.batch + T - 1) / T;
+  const int li = lane & 15, lk = lane >> 4;
+  const int ub = 16 * wave;  // the wave's unit tile
+  // heads' lane roles: wave w, samples 8 w + (lane & 7); actor lanes (d = (lane >> 3) & 1, quarter
+  // q = lane >> 4 of the 64 inputs), critic lanes (eighth q = lane >> 3)
+  const int hs = 8 * wave + (lane & 7);
+  float xg[10];
+  float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto loads = [&](int tile) __attribute__((always_inline)) {
+    // unconditional loads from valid addresses (a clamped sample and input), zeros selected after:
+    // conditional loads compile to exec-masked branches that wait for each load in turn
+    const int s0 = tile * T, nvalid = min(T, A.batch - s0);
+    const int r = tid >> 3, q = tid & 7;
+    const float* row = A.obs_rows + (size_t)A.idx[s0 + min(r, nvalid - 1)] * NOBS;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      const int k = q * 10 + i;
+      const float v = row[min(k, NOBS - 1)];
+      xg[i] = (r < nvalid && k < NOBS) ? v : 0.0f;
+    }
+    const int sidx = A.idx[s0 + min(hs, nvalid - 1)];
+    const bool hv = hs < nvalid;
+    if (net == 0) {
+      const float2 a = *reinterpret_cast<const float2*>(A.actions + 2 * (size_t)sidx);
+      const float o = A.old_logp[sidx], ad = A.adv[sidx];
+      hin[0] = hv ? a.x : 0.0f;
+      hin[1] = hv ? a.y : 0.0f;
+      hin[2] = hv ? o : 0.0f;
+      hin[3] = hv ? ad : 0.0f;
+    } else {
+      const float rt = A.ret[sidx];
+      hin[0] = hv ? rt : 0.0f;
+    }
+  };
+
+  if (tile0 < ntiles) loads(tile0);
+  stage_net(A.params, w, net);
+
+  f4v gw1[5], gw2[4];
+#pragma unroll
+  for (int j = 0; j < 5; j++) gw1[j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int j = 0; j < 4; j++) gw2[j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+  float accv[2] = {0.0f, 0.0f};  // vector items tid and tid + 256 (vec_item_g1)
+  float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
+
+  for (int tile = tile0; tile < ntiles; tile += tstride) {
+    // an opaque zero per tile: every LDS address below depends on it, so none is hoisted out of the
+    // tile loop (the hoisted swizzled addresses filled the register file and spilled)
+    int zo = 0;
+    asm volatile("" : "+v"(zo));
+    float* tb = tl + zo;
+    const float* wb = tb;
+    const int s0 = tile * T, nvalid = min(T, A.batch - s0);
+    __syncthreads();  // the previous tile's LDS reads are done (and the weights staged)
+    if (tile != tile0) loads(tile);
+    {
+      const int r = tid >> 3, q = tid & 7;
+#pragma unroll
+      for (int i = 0; i < 10; i++) tb[X + (q * 10 + i) * LDP + r] = xg[i];
+    }
+    __syncthreads();
+    PSTAMP(1);
+    {  // layer 1: H1 [64 x 32] = tanh(W1 X + b1)
+      f4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < 80; k0 += 4) {
+        const int k = k0 + lk;
+        const float wa = wb[w1t(k, ub + li)];
+        a0 = mfma4(wa, tb[X + k * LDP + li], a0);
+        a1 = mfma4(wa, tb[X + k * LDP + 16 + li], a1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int u = ub + 4 * lk + r;
+        const float bb = wb[B1 + u];
+        tb[H1 + u * LDP + li] = ftanh(a0[r] + bb);
+        tb[H1 + u * LDP + 16 + li] = ftanh(a1[r] + bb);
+      }
+    }
+    __syncthreads();
+    PSTAMP(2);
+    {  // layer 2: H2 [64 x 32] = tanh(W2 H1 + b2)
+      f4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;
+        const float wa = wb[w2(ub + li, k)];
+        a0 = mfma4(wa, tb[H1 + k * LDP + li], a0);
+        a1 = mfma4(wa, tb[H1 + k * LDP + 16 + li], a1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int u = ub + 4 * lk + r;
+        const float bb = wb[B2 + u];
+        tb[H2 + u * LDP + li] = ftanh(a0[r] + bb);
+        tb[H2 + u * LDP + 16 + li] = ftanh(a1[r] + bb);
+      }
+    }
+    __syncthreads();
+    PSTAMP(3);
+    const bool hvalid = hs < nvalid;
+    if (net == 0) {  // actor heads: mu[d] of sample hs, a 16-term quarter per lane, butterflies over q
+      const int d = (lane >> 3) & 1, q = lane >> 4;
+      float m = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {  // k order rotated by 2q: the four quarters' H2 reads hit distinct banks
+        const int k = 16 * q + ((j + 2 * q) & 15);
+        m = fmaf(wb[HW + d * H + k], tb[H2 + k * LDP + hs], m);
+      }
+      m += __shfl_xor(m, 16, 64);
+      m += __shfl_xor(m, 32, 64);
+      m += wb[HB + d];
+      const float mo = __shfl_xor(m, 8, 64);  // the other dimension's mean
+      const float mu0 = d ? mo : m, mu1 = d ? m : mo;
+      const float ls0 = wb[HB + 2], ls1 = wb[HB + 3];
+      const float logp = gauss_term(hin[0], mu0, ls0) + gauss_term(hin[1], mu1, ls1);
+      const float lr = logp - hin[2];
+      const float r = fexp(lr);
+      const float adv = (hin[3] - A.stats[0]) * A.stats[1];
+      const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
+      const float l1 = adv * r, l2 = adv * rc;
+      // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
+      // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
+      const float glogp = hvalid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
+      if (q == 0) {
+        const float ls = d ? ls1 : ls0, mu = d ? mu1 : mu0, ad = d ? hin[1] : hin[0];
+        const float inv_var = fexp(-2.0f * ls);
+        const float dv = ad - mu;
+        tb[GA + d * LDP + hs] = glogp * dv * inv_var;
+        tb[GA + (2 + d) * LDP + hs] = glogp * (dv * dv * inv_var - 1.0f);
+        if (d == 0 && hvalid) {
+          la += -fminf(l1, l2);
+          lb += (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
+          lc += (r - 1.0f) - lr;
+          ln += 1.0f;
+        }
+      }
+    } else {  // critic head: V of sample hs, an 8-term eighth per lane
+      const int q = lane >> 3;
+      float v = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {  // k order rotated by 2q: the eight groups' H2 reads hit distinct banks
+        const int k = 8 * q + ((j + 2 * q) & 7);
+        v = fmaf(wb[HW + k], tb[H2 + k * LDP + hs], v);
+      }
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      v += wb[HB];
+      if (q == 0) {
+        const float R = hin[0];
+        tb[GA + hs] = hvalid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
+        if (hvalid) la += (R - v) * (R - v);
+      }
+    }
+    __syncthreads();
+    PSTAMP(4);
+    {  // D2 = dL/dH2 (1 - H2^2): thread (unit tid >> 2, samples 8 (tid & 3) ...)
+      const int u = tid >> 2, c0 = 8 * (tid & 3);
+      const float ha = wb[HW + u], hb = net ? 0.0f : wb[HW + H + u];
+#pragma unroll
+      for (int c = c0; c < c0 + 8; c += 4) {
+        const float4 h2 = *reinterpret_cast<const float4*>(tb + H2 + u * LDP + c);
+        const float4 g0 = *reinterpret_cast<const float4*>(tb + GA + c);
+        float4 dh;
+        if (net == 0) {
+          const float4 g1v = *reinterpret_cast<const float4*>(tb + GA + LDP + c);
+          dh = make_float4(g0.x * ha + g1v.x * hb, g0.y * ha + g1v.y * hb, g0.z * ha + g1v.z * hb, g0.w * ha + g1v.w * hb);
+        } else {
+          dh = make_float4(g0.x * ha, g0.y * ha, g0.z * ha, g0.w * ha);
+        }
+        *reinterpret_cast<float4*>(tb + D2 + u * LDP + c) =
+            make_float4(dh.x * (1.0f - h2.x * h2.x), dh.y * (1.0f - h2.y * h2.y), dh.z * (1.0f - h2.z * h2.z),
+                        dh.w * (1.0f - h2.w * h2.w));
+      }
+    }
+    __syncthreads();
+    PSTAMP(5);
+    f4v d1a = {0.f, 0.f, 0.f, 0.f}, d1b = {0.f, 0.f, 0.f, 0.f};
+    {  // W2^T D2 for the wave's layer-1 units, and gW2 [64 x 64] += D2 H1^T (rows = the wave's units)
+#pragma unroll
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;  // layer-2 unit
+        const float wt = wb[w2(k, ub + li)];
+        d1a = mfma4(wt, tb[D2 + k * LDP + li], d1a);
+        d1b = mfma4(wt, tb[D2 + k * LDP + 16 + li], d1b);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // scheduling regions: bounded register pressure
+#pragma unroll
+      for (int q0 = 0; q0 < T; q0 += 4) {
+        const int q = q0 + lk;  // sample
+        const float a = tb[D2 + (ub + li) * LDP + q];
+#pragma unroll
+        for (int j = 0; j < 4; j++) gw2[j] = mfma4(a, tb[H1 + (16 * j + li) * LDP + q], gw2[j]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // vector items read before D1 replaces H1 (vec_item_g1): b2 and the heads
+#pragma unroll
+    for (int bb = 0; bb < 2; bb++) {
+      const int i = tid + bb * GRAD_THREADS;
+      if (i >= 64 && i < (net ? G1_NVC : G1_NVA)) accv[bb] += vec_item_g1(tb, net, i);
+    }
+    __syncthreads();  // every read of H1 (gW2) and H2 is done: D1 may replace H1
+    PSTAMP(6);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int u = ub + 4 * lk + r;
+      const float h1a = tb[H1 + u * LDP + li], h1b = tb[H1 + u * LDP + 16 + li];
+      tb[H1 + u * LDP + li] = d1a[r] * (1.0f - h1a * h1a);
+      tb[H1 + u * LDP + 16 + li] = d1b[r] * (1.0f - h1b * h1b);
+    }
+    __syncthreads();
+    PSTAMP(7);
+    // gW1 [64 x 80] += D1 X^T (rows = the wave's units); b1 = the row sums of D1
+#pragma unroll
+    for (int q0 = 0; q0 < T; q0 += 4) {
+      const int q = q0 + lk;
+      const float a = tb[H1 + (ub + li) * LDP + q];
+#pragma unroll
+      for (int j = 0; j < 5; j++) gw1[j] = mfma4(a, tb[X + (16 * j + li) * LDP + q], gw1[j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (tid < H) accv[0] += vec_item_g1(tb, net, tid);
+  }
+  PSTAMP(8);
+  // this workgroup's half of partial row tile0: its net's weight gradients and vector items
+  const int row = tile0;
+  float* g = A.gpart + (size_t)row * P;
+  {
+    const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int u = ub + 4 * lk + r;
+#pragma unroll
+      for (int j = 0; j < 5; j++)
+        if (16 * j + li < NOBS) g[ow1 + u * NOBS + 16 * j + li] = gw1[j][r];
+#pragma unroll
+      for (int j = 0; j < 4; j++) g[ow2 + u * H + 16 * j + li] = gw2[j][r];
+    }
+  }
+#pragma unroll
+  for (int bb = 0; bb < 2; bb++) {
+    const int i = tid + bb * GRAD_THREADS;
+    if (i < (net ? G1_NVC : G1_NVA)) g[vec_offset_g1(net, i)] = accv[bb];
+  }
+  // loss sums: per wave, then the four waves in order through LDS (the tile is done)
+  la = wave_sum(la);
+  lb = wave_sum(lb);
+  lc = wave_sum(lc);
+  ln = wave_sum(ln);
+  __syncthreads();
+  if (lane == 0) {
+    tl[X + 4 * wave + 0] = la;
+    tl[X + 4 * wave + 1] = lb;
+    tl[X + 4 * wave + 2] = lc;
+    tl[X + 4 * wave + 3] = ln;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    const float s = (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]);
+    float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
+    if (net == 0) {
+      lp[tid == 0 ? 0 : tid + 1] = s;  // policy loss, clipped count, approx-kl sum, samples
+      if (tid == 0) lp[5] = lp[6] = lp[7] = 0.0f;
+    } else if (tid == 0) {
+      lp[1] = s;  // value loss sum
+    }
+  }
+  PSTAMP(15);
+}
+
 // ---- ackppo_act: MFMA policy tile. 16 envs per 256-lane workgroup (4096 envs = 256 workgroups,
 // one per CU): the weights are staged as in ackppo_grad (transposed / swizzled), X [80][16],
 // H1 / H2 [128 units][16 envs] in LDS; wave w computes unit tiles 2w, 2w + 1 of both layers as
@@ -1040,6 +1457,7 @@ int launched(const char* what) {
   return ACKPPO_OK;
 }
 constexpr size_t GRAD_LDS = (size_t)G_TOTAL * sizeof(float);
+constexpr size_t GRAD1_LDS = (size_t)g1::TOTAL * sizeof(float);
 // hipFuncSetAttribute is applied per device: flags indexed by the caller's current device
 constexpr int MAX_DEV = 64;
 bool g_grad_attr[MAX_DEV] = {};
@@ -1196,16 +1614,20 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
     return fail(ACKPPO_EINVAL, "ackppo_grad: bad arguments");
   const int dev = current_device();
   if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
+  const void* kern = AK_PPO_GRAD1 ? (const void*)ackppo_grad1_kernel : (const void*)ackppo_grad_kernel;
+  const size_t lds = AK_PPO_GRAD1 ? GRAD1_LDS : GRAD_LDS;
   if (!g_grad_attr[dev]) {
-    const hipError_t e = hipFuncSetAttribute((const void*)ackppo_grad_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS);
-    if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the 158 KiB LDS footprint");
+    const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
     g_grad_attr[dev] = true;
   }
   GradArgs A{params, obs_rows, actions, old_log_prob, advantages, returns, idx, batch, stats, clip_range, ent_coef,
              vf_coef, grad_partial, loss_partial};
-  hipLaunchKernelGGL(ackppo_grad_kernel, dim3(ackppo_grad_blocks(batch)), dim3(GRAD_THREADS), GRAD_LDS,
-                     (hipStream_t)stream, A);
+  const int nblk = ackppo_grad_blocks(batch);  // partial rows
+  if (AK_PPO_GRAD1)  // two workgroups (actor, critic) per partial row
+    hipLaunchKernelGGL(ackppo_grad1_kernel, dim3(2 * nblk), dim3(GRAD_THREADS), lds, (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(ackppo_grad_kernel, dim3(nblk), dim3(GRAD_THREADS), lds, (hipStream_t)stream, A);
   return launched("ackppo_grad");
 }
 
@@ -1274,6 +1696,139 @@ int ackppo_epoch(float* params, const float* obs_rows, const float* actions, con
     if (rc) return rc;
   }
   return ACKPPO_OK;
+}
+
+
+int ackppo_train(const ackppo_train_desc* d, void* stream) {
+  if (!d || !d->obs_rows || !d->actions || !d->old_log_prob || !d->advantages || !d->returns || !d->params ||
+      !d->exp_avg || !d->exp_avg_sq || !d->perm || !d->stats || !d->grad_partial || !d->loss_partial || !d->grad ||
+      !d->loss_acc || d->n_idx < 0 || d->batch <= 0 || d->n_epochs < 0 || d->adam_step0 < 0 || d->world < 1)
+    return fail(ACKPPO_EINVAL, "ackppo_train: bad arguments");
+  // the data-parallel sequence whenever there is a hook (world 1 with a hook: its collectives reduce
+  // over one rank -- the same path, timed on one GPU)
+  const bool dp = d->allreduce != nullptr;
+  if ((d->world > 1 && !dp) || (dp && !d->moments))
+    return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
+  const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
+    return fail(ACKPPO_EHIP, "ackppo_train: hipMemsetAsync(loss_acc)");
+  if (S == 0) return ACKPPO_OK;
+  const float scale = 1.0f / (float)d->world;
+  int rc;
+  auto coll = [&](void* buf, int64_t count, int dtype, const char* what) -> int {
+    g_err[0] = 0;
+    const int r = d->allreduce(buf, count, dtype, d->allreduce_user, stream);
+    if (r) {
+      char why[sizeof g_err];
+      snprintf(why, sizeof why, "%s", g_err);  // the hook's own message, if it left one
+      snprintf(g_err, sizeof g_err, "ackppo_train: %s all-reduce failed (%d) %s", what, r, why);
+      return ACKPPO_EHIP;
+    }
+    return ACKPPO_OK;
+  };
+  for (int ep = 0; ep < d->n_epochs; ep++) {
+    if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
+    if (!dp) {
+      if ((rc = ackppo_adv_stats(d->advantages, d->perm, S, B, d->normalize_advantage, d->stats, stream))) return rc;
+    } else {
+      double* mom = d->moments;
+      if ((rc = ackppo_adv_moments(d->advantages, d->perm, S, B, 0, mom, stream))) return rc;
+      if ((rc = coll(mom, 2 * (int64_t)nmb, ACKPPO_F64, "advantage count/sum"))) return rc;
+      if ((rc = ackppo_adv_moments(d->advantages, d->perm, S, B, 1, mom, stream))) return rc;
+      if ((rc = coll(mom + 2 * nmb, nmb, ACKPPO_F64, "advantage deviation"))) return rc;
+      if ((rc = ackppo_adv_finalize(mom, nmb, d->normalize_advantage, d->stats, stream))) return rc;
+    }
+    for (int m = 0; m < nmb; m++) {
+      const int nb = S - m * B < B ? S - m * B : B;
+      if ((rc = ackppo_grad(d->params, d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns,
+                            d->perm + (size_t)m * B, nb, d->stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef,
+                            d->grad_partial, d->loss_partial, stream)))
+        return rc;
+      if ((rc = reduce_launch(d->grad_partial, d->loss_partial, ackppo_grad_blocks(nb), d->ent_coef, d->grad,
+                              d->loss_acc, 1, stream)))
+        return rc;
+      if (dp && (rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
+      const double t = (double)(d->adam_step0 + (int64_t)ep * nmb + m + 1);  // torch's bias corrections (float64)
+      if ((rc = ackppo_adam(d->params, d->grad, d->exp_avg, d->exp_avg_sq, scale, d->max_grad_norm, (float)d->beta1,
+                            (float)d->beta2, d->eps, (float)(d->learning_rate / (1.0 - pow(d->beta1, t))),
+                            (float)sqrt(1.0 - pow(d->beta2, t)), d->grad_norm_out, stream)))
+        return rc;
+    }
+  }
+  return ACKPPO_OK;
+}
+
+// ---- native RCCL: the process's own librccl.so.1 (torch's, when it is loaded), opened at run time
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init = nullptr;
+  decltype(&ncclAllReduce) allreduce = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) errstr = nullptr;
+  bool ok = false;
+};
+Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // already in the process (torch)
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!h) return x;
+    x.get_id = (decltype(x.get_id))dlsym(h, "ncclGetUniqueId");
+    x.init = (decltype(x.init))dlsym(h, "ncclCommInitRank");
+    x.allreduce = (decltype(x.allreduce))dlsym(h, "ncclAllReduce");
+    x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+    x.errstr = (decltype(x.errstr))dlsym(h, "ncclGetErrorString");
+    x.ok = x.get_id && x.init && x.allreduce && x.destroy && x.errstr;
+    return x;
+  }();
+  return r;
+}
+int rccl_fail(const char* what, ncclResult_t r) {
+  snprintf(g_err, sizeof g_err, "%s: %s", what, rccl().errstr ? rccl().errstr(r) : "RCCL error");
+  return ACKPPO_EHIP;
+}
+}  // namespace
+
+int ackppo_rccl_unique_id(void* id128) {
+  if (!id128) return fail(ACKPPO_EINVAL, "ackppo_rccl_unique_id: bad arguments");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_unique_id: librccl.so.1 not loadable");
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  ncclUniqueId id;
+  const ncclResult_t r = rccl().get_id(&id);
+  if (r != ncclSuccess) return rccl_fail("ncclGetUniqueId", r);
+  memcpy(id128, &id, sizeof id);
+  return ACKPPO_OK;
+}
+
+int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm) {
+  if (!id128 || !comm || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(ACKPPO_EINVAL, "ackppo_rccl_init: bad arguments");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_init: librccl.so.1 not loadable");
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof id);
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = rccl().init(&c, nranks, id, rank);
+  if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);
+  *comm = c;
+  return ACKPPO_OK;
+}
+
+int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void* stream) {
+  if (!buf || !comm || count < 0 || (dtype != ACKPPO_F32 && dtype != ACKPPO_F64))
+    return fail(ACKPPO_EINVAL, "ackppo_rccl_allreduce: bad arguments");
+  const ncclResult_t r = rccl().allreduce(buf, buf, (size_t)count, dtype == ACKPPO_F32 ? ncclFloat32 : ncclFloat64,
+                                          ncclSum, (ncclComm_t)comm, (hipStream_t)stream);
+  return r == ncclSuccess ? ACKPPO_OK : rccl_fail("ncclAllReduce", r);
+}
+
+int ackppo_rccl_destroy(void* comm) {
+  if (!comm) return ACKPPO_OK;
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_destroy: librccl.so.1 not loadable");
+  const ncclResult_t r = rccl().destroy((ncclComm_t)comm);
+  return r == ncclSuccess ? ACKPPO_OK : rccl_fail("ncclCommDestroy", r);
 }
 
 }  // extern "C"

@@ -5,12 +5,12 @@ The reference trains with stable-baselines3 `PPO('MlpPolicy', DummyVecEnv([Monit
 `predict` / `save` surface and its semantics, but every per-sample computation runs in
 libackppo.so (include/ackppo.h) on the GPU, next to the env step:
 
-  rollout step : ackppo_act (policy -> action, log_prob, value, obs row)  -> ackphys_step
-                 (auto-reset) -> ackppo_bootstrap (TimeLimit bootstrap, done flags)
-  after rollout: ackppo_value (last values) -> ackppo_gae
-  each epoch   : one device permutation (ackppo_permutation, the SB3 minibatch shuffle),
-                 advantage statistics for all minibatches (ackppo_adv_stats)
-  minibatch    : ackppo_grad -> ackppo_reduce -> [RCCL all-reduce of 75 KB] -> ackppo_adam
+  rollout      : one ackphys_ppo_rollout launch (policy + env steps + TimeLimit bootstrap fused), or
+                 per step ackppo_act (policy -> action, log_prob, value, obs row) -> ackphys_step
+                 (auto-reset) -> ackppo_bootstrap; then ackppo_value (last values) -> ackppo_gae
+  train()      : ONE ackppo_train call (include/ackppo.h), which enqueues for each epoch the device
+                 permutation (the SB3 minibatch shuffle) and the advantage statistics, then per
+                 minibatch ackppo_grad -> ackppo_reduce -> [all-reduce of 75 KB] -> ackppo_adam
 
 Nothing leaves the device inside `learn` except the logging scalars at the end of an update.
 Torch tensors are the buffer container only.
@@ -20,7 +20,11 @@ Data-parallel (one process per GPU, torchrun): every rank steps its own env shar
 summed over ranks with one all-reduce; the Adam kernel scales by 1/world. A minibatch is then
 world x batch_size samples, split evenly over ranks, and its advantages are normalised with the
 statistics of all world x batch_size samples (ackppo_adv_moments: two small all-reduces of the
-per-minibatch count / sum / squared deviations per epoch), as one SB3 learner would.
+per-minibatch count / sum / squared deviations per epoch), as one SB3 learner would. The
+collectives are enqueued from C by ackppo_train through a hook (shard.TrainerCollective): a native
+RCCL communicator (ackppo_rccl_allreduce) on GPU nodes, a host-staged torch.distributed callback in
+gloo rehearsals -- per iteration n_epochs x (nmb + 2) all-reduces, none of them a host round trip
+on the RCCL path.
 """
 from __future__ import annotations
 
@@ -105,7 +109,7 @@ class PPO:
                  clip_range_vf=None, normalize_advantage: bool = True, ent_coef: float = 0.0, vf_coef: float = 0.5,
                  max_grad_norm: float = 0.5, target_kl=None, seed: int | None = None, verbose: int = 0,
                  policy_kwargs: dict | None = None, device=None, world: int | None = None, rank: int | None = None,
-                 fused_rollout: bool | None = None):
+                 fused_rollout: bool | None = None, collective: str | None = None):
         if policy != "MlpPolicy":
             raise ValueError("only 'MlpPolicy' (the reference's policy, train.py:126) is provided")
         if clip_range_vf is not None or target_kl is not None:
@@ -160,7 +164,6 @@ class PPO:
         self.grad = torch.zeros(NPARAM, **f32)
         self.loss = torch.zeros(NLOSS, **f32)
         self.loss_acc = torch.zeros(NLOSS, **f32)
-        self.fused_epoch = True  # world 1: ackppo_epoch (same kernels and scalars as the per-minibatch calls)
         self.gnorm = torch.zeros(1, **f32)
         nmb = (T * N + batch_size - 1) // batch_size
         self.mb_stats = torch.zeros(nmb, 2, **f32)
@@ -169,6 +172,13 @@ class PPO:
         self.perm_key = (self.seed * 7919 + self.rank) & 0xFFFFFFFFFFFFFFFF
         self.perm_epoch = 0
         self.perm = torch.empty(self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
+        # the all-reduce hook of the data-parallel update: RCCL (native communicator) on GPU nodes,
+        # host-staged in gloo rehearsals; collective="rccl" at world 1 runs the data-parallel path over
+        # a one-rank communicator (timing that path on one GPU)
+        self.collective = None
+        self._desc = self._train_desc()
+        if self.world > 1 or collective is not None:
+            self.set_collective(collective)
         self.num_timesteps = 0
         self.episodes_total = 0
         self._rollout_step = 0
@@ -270,45 +280,50 @@ class PPO:
         _lib.ppo_check(L.ackppo_value(_ptr(self.params), _ptr(sim.obs_soa), N, _ptr(self.last_values), s),
                        "ackppo_value")
 
+    def _train_desc(self):
+        """ackppo_train_desc with every pointer of this learner (the buffers are never reallocated)."""
+        d = _lib.TrainDesc()
+        d.obs_rows, d.actions, d.old_log_prob = (t.data_ptr() for t in (self.buf_obs, self.buf_act, self.buf_logp))
+        d.advantages, d.returns = self.buf_adv.data_ptr(), self.buf_ret.data_ptr()
+        d.n_idx, d.batch = self.n_steps * self.n_envs, self.batch_size
+        d.params, d.exp_avg, d.exp_avg_sq = (t.data_ptr() for t in (self.params, self.exp_avg, self.exp_avg_sq))
+        d.perm, d.stats, d.moments = self.perm.data_ptr(), self.mb_stats.data_ptr(), self.mb_moments.data_ptr()
+        d.grad_partial, d.loss_partial = self.gpart.data_ptr(), self.lpart.data_ptr()
+        d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
+        d.world = self.world
+        return d
+
+    def set_collective(self, kind: str | None):
+        """The update's all-reduce hook (shard.TrainerCollective): "rccl", "host", None = the
+        backend's default at world > 1, or no hook at all at world 1."""
+        if self.collective is not None:
+            self.collective.close()
+            self.collective = None
+        d = self._desc
+        d.allreduce, d.allreduce_user = None, None
+        if self.world == 1 and kind is None:
+            return
+        c = shard.TrainerCollective(self.world, self.device, kind=kind)
+        c.register(self.grad)
+        c.register(self.mb_moments[0:2].reshape(-1))
+        c.register(self.mb_moments[2])
+        self.collective = c
+        d.allreduce, d.allreduce_user = c.fn.value, c.user
+
     def train(self):
-        L, s = self.L, self._stream()
+        """SB3 PPO.train: n_epochs over shuffled minibatches -- ONE ackppo_train call (every launch
+        and collective of the update enqueued from C), then the logging scalars."""
+        d = self._desc
         S, B = self.n_steps * self.n_envs, self.batch_size
         nmb = (S + B - 1) // B
-        self.loss_acc.zero_()
-        b1, b2 = 0.9, 0.999
-        for _ in range(self.n_epochs):
-            _lib.ppo_check(L.ackppo_permutation(S, self.perm_key, self.perm_epoch, _ptr(self.perm), s),
-                           "ackppo_permutation")
-            self.perm_epoch += 1
-            perm = self.perm
-            self._advantage_stats(perm, S, B)
-            if self.world == 1 and self.fused_epoch:  # one C call per epoch: grad -> reduce -> adam per minibatch
-                _lib.ppo_check(L.ackppo_epoch(_ptr(self.params), _ptr(self.buf_obs), _ptr(self.buf_act),
-                                              _ptr(self.buf_logp), _ptr(self.buf_adv), _ptr(self.buf_ret), _ptr(perm),
-                                              S, B, _ptr(self.mb_stats), self.clip_range, self.ent_coef, self.vf_coef,
-                                              self.max_grad_norm, self.learning_rate, b1, b2, 1e-5, self.adam_step,
-                                              _ptr(self.gpart), _ptr(self.lpart), _ptr(self.grad),
-                                              _ptr(self.loss_acc), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
-                                              _ptr(self.gnorm), s), "ackppo_epoch")
-                self.adam_step += nmb
-                continue
-            for m in range(nmb):
-                nb = min(B, S - m * B)
-                idx = perm[m * B:]
-                _lib.ppo_check(L.ackppo_grad(_ptr(self.params), _ptr(self.buf_obs), _ptr(self.buf_act),
-                                             _ptr(self.buf_logp), _ptr(self.buf_adv), _ptr(self.buf_ret), _ptr(idx),
-                                             nb, _ptr(self.mb_stats[m]), self.clip_range, self.ent_coef, self.vf_coef,
-                                             _ptr(self.gpart), _ptr(self.lpart), s), "ackppo_grad")
-                _lib.ppo_check(L.ackppo_reduce(_ptr(self.gpart), _ptr(self.lpart), L.ackppo_grad_blocks(nb),
-                                               self.ent_coef, _ptr(self.grad), _ptr(self.loss), s), "ackppo_reduce")
-                shard.all_reduce_sum_(self.grad, self.world)
-                self.adam_step += 1
-                t = self.adam_step
-                _lib.ppo_check(L.ackppo_adam(_ptr(self.params), _ptr(self.grad), _ptr(self.exp_avg),
-                                             _ptr(self.exp_avg_sq), 1.0 / self.world, self.max_grad_norm, b1, b2,
-                                             1e-5, self.learning_rate / (1 - b1 ** t), math.sqrt(1 - b2 ** t),
-                                             _ptr(self.gnorm), s), "ackppo_adam")
-                self.loss_acc.add_(self.loss)
+        d.n_epochs, d.perm_key, d.perm_epoch0 = self.n_epochs, self.perm_key, self.perm_epoch
+        d.normalize_advantage = int(self.normalize_advantage)
+        d.clip_range, d.ent_coef, d.vf_coef, d.max_grad_norm = (self.clip_range, self.ent_coef, self.vf_coef,
+                                                                self.max_grad_norm)
+        d.learning_rate, d.beta1, d.beta2, d.eps, d.adam_step0 = self.learning_rate, 0.9, 0.999, 1e-5, self.adam_step
+        _lib.ppo_check(self.L.ackppo_train(C.byref(d), self._stream()), "ackppo_train")
+        self.perm_epoch += self.n_epochs
+        self.adam_step += self.n_epochs * nmb
         la = self.loss_acc.cpu().tolist()
         n = max(la[4], 1.0)
         log_std = self.params[:2].detach().cpu()
@@ -317,21 +332,6 @@ class PPO:
                        "train/entropy_loss": -float((0.5 + 0.5 * math.log(2 * math.pi) + log_std).sum()),
                        "train/std": float(log_std.exp().mean()), "train/n_updates": self.adam_step,
                        "train/grad_norm": float(self.gnorm.item())}
-
-    def _advantage_stats(self, perm, S: int, B: int):
-        """mb_stats[m] = (mean, 1/(std+1e-8)) of world minibatch m (SB3 normalize_advantage)."""
-        L, s = self.L, self._stream()
-        if self.world == 1:
-            _lib.ppo_check(L.ackppo_adv_stats(_ptr(self.buf_adv), _ptr(perm), S, B, int(self.normalize_advantage),
-                                              _ptr(self.mb_stats), s), "ackppo_adv_stats")
-            return
-        mom = self.mb_moments
-        _lib.ppo_check(L.ackppo_adv_moments(_ptr(self.buf_adv), _ptr(perm), S, B, 0, _ptr(mom), s), "ackppo_adv_moments")
-        shard.all_reduce_sum_(mom[0:2], self.world)
-        _lib.ppo_check(L.ackppo_adv_moments(_ptr(self.buf_adv), _ptr(perm), S, B, 1, _ptr(mom), s), "ackppo_adv_moments")
-        shard.all_reduce_sum_(mom[2], self.world)
-        _lib.ppo_check(L.ackppo_adv_finalize(_ptr(mom), mom.shape[1], int(self.normalize_advantage),
-                                             _ptr(self.mb_stats), s), "ackppo_adv_finalize")
 
     def learn(self, total_timesteps: int, callback=None, log_interval: int = 1, reset_num_timesteps: bool = True,
               progress_bar: bool = False):

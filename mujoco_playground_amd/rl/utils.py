@@ -1,5 +1,6 @@
-"""Evaluation helpers with the reference's API (src/rl/utils.py:8-50), which train.py calls after
-training (`from rl.utils import evaluate_agent`, train.py:313), plus a batched evaluation over an
+"""Evaluation helpers with the reference's API (src/rl/utils.py:8-72): evaluate_agent /
+compute_episode_stats, which train.py calls after training (`from rl.utils import evaluate_agent`,
+train.py:313), normalize_observation and create_action_mapping, plus a batched evaluation over an
 AckermannVecEnv (every env runs one episode in the same HIP launches).
 """
 from __future__ import annotations
@@ -61,3 +62,22 @@ def evaluate_vec(venv, policy, max_steps: int | None = None) -> dict:
     out = compute_episode_stats(ret.cpu().numpy(), length.cpu().numpy())
     out["success_rate"] = float(success.float().mean().item())
     return out
+
+
+def normalize_observation(obs, obs_space):
+    """(obs - low) / (high - low) per entry for a Box space (zero-width entries divide by 1); any
+    other space returns obs unchanged (utils.py:53-63)."""
+    if not (hasattr(obs_space, "low") and hasattr(obs_space, "high")):
+        return obs
+    low = np.asarray(obs_space.low)
+    span = np.asarray(obs_space.high) - low
+    span = np.where(span == 0, 1.0, span).astype(span.dtype)
+    return (obs - low) / span
+
+
+def create_action_mapping(action_space, max_linear: float = 1.0, max_angular: float = 1.0):
+    """A function mapping a normalised action [2] to (linear_x, angular_z) = (a0 * max_linear,
+    a1 * max_angular) (utils.py:66-72; action_space is unused there too)."""
+    def map_action(action):
+        return action[0] * max_linear, action[1] * max_angular
+    return map_action

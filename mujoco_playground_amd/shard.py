@@ -96,6 +96,74 @@ def all_reduce_sum_(t: torch.Tensor, world: int) -> torch.Tensor:
     return t
 
 
+class TrainerCollective:
+    """The all-reduce hook libackppo's ackppo_train calls between a minibatch's gradient and its Adam
+    step (include/ackppo.h ackppo_allreduce_fn), so a data-parallel PPO update is one C call per
+    train() with no per-minibatch host round trip.
+
+    kind "rccl": a native RCCL communicator of libackppo (ackppo_rccl_*) over the ranks of the
+      default process group (its unique id broadcast once over that group), or over this process
+      alone at world 1 (a one-rank communicator: the data-parallel path with real RCCL calls, for
+      timing it on one GPU); the hook is ackppo_rccl_allreduce itself, so each collective is
+      enqueued from C.
+    kind "host": a Python callback that all-reduces through torch.distributed on host copies --
+      the gloo rehearsals (several ranks on one device, where RCCL cannot run); the callback
+      synchronises the stream, so it is the slow path, for tests only.
+    Buffers handed to the "host" hook must be registered (`register`)."""
+
+    def __init__(self, world: int, device, kind: str | None = None):
+        import ctypes as C
+
+        from . import _lib
+        self.world, self.device = world, device
+        self.kind = kind or ("host" if _backend_is_gloo() else "rccl")
+        self.L = _lib.ppo_lib()
+        self._bufs = {}
+        self.comm = C.c_void_p()
+        if self.kind == "rccl":
+            idb = (C.c_char * 128)()
+            rank = dist.get_rank() if world > 1 else 0
+            if rank == 0:
+                _lib.ppo_check(self.L.ackppo_rccl_unique_id(idb), "ackppo_rccl_unique_id")
+            if world > 1:
+                t = torch.frombuffer(bytearray(bytes(idb)), dtype=torch.uint8).to(device)
+                dist.broadcast(t, 0)
+                idb = (C.c_char * 128).from_buffer_copy(bytes(t.cpu().numpy()))
+            _lib.ppo_check(self.L.ackppo_rccl_init(idb, world, rank, C.byref(self.comm)), "ackppo_rccl_init")
+            self.fn = C.cast(self.L.ackppo_rccl_allreduce, C.c_void_p)
+            self.user = self.comm
+        elif self.kind == "host":
+            def hook(buf, count, dtype, user, stream):
+                try:
+                    t = self._bufs[(buf, count, dtype)]
+                    all_reduce_sum_(t, self.world)
+                    return 0
+                except Exception as e:  # noqa: BLE001 -- reported through the C return code
+                    print(f"TrainerCollective host hook: {e!r}", flush=True)
+                    return -1
+            self._cb = _lib.ALLREDUCE_FN(hook)  # kept alive with the collective
+            self.fn = C.cast(self._cb, C.c_void_p)
+            self.user = None
+        else:
+            raise ValueError(f"unknown collective kind {kind!r}")
+
+    def register(self, t: torch.Tensor):
+        """A contiguous buffer the trainer all-reduces (host hook lookup by pointer, count, dtype)."""
+        dtype = {torch.float32: 0, torch.float64: 1}[t.dtype]
+        self._bufs[(t.data_ptr(), t.numel(), dtype)] = t
+
+    def close(self):
+        if self.kind == "rccl" and self.comm:
+            self.L.ackppo_rccl_destroy(self.comm)
+            self.comm = type(self.comm)()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 def broadcast_(t: torch.Tensor, world: int, src: int = 0) -> torch.Tensor:
     if world == 1:
         return t

@@ -182,12 +182,23 @@ class BatchedAckermannSim:
                 self.terminal_obs_soa.copy_(torch.where(done[None, :], tobs[-1], self.terminal_obs_soa))
         return obs, rew, term, trunc
 
+    def rollout_buffers(self, k_steps: int, want_info: bool = False, want_terminal: bool = False) -> dict:
+        """Preallocated per-step output slices for `rollout_launcher(..., outputs=...)`: obs
+        [K,79,N], reward [K,N], term, trunc [K,N] (uint8), info [K,4,N] / terminal obs [K,79,N]
+        when asked for (a rollout buffer a consumer of every step's observation reads)."""
+        f32, u8, d, n, k = torch.float32, torch.uint8, self.device, self.n, int(k_steps)
+        return {"obs": torch.empty(k, NOBS, n, dtype=f32, device=d), "reward": torch.empty(k, n, dtype=f32, device=d),
+                "term": torch.empty(k, n, dtype=u8, device=d), "trunc": torch.empty(k, n, dtype=u8, device=d),
+                "terminal_obs": torch.zeros(k, NOBS, n, dtype=f32, device=d) if want_terminal else None,
+                "info": torch.empty(k, 4, n, dtype=f32, device=d) if want_info else None}
+
     def rollout_launcher(self, actions: torch.Tensor, autoreset: bool = True, want_info: bool = False,
-                         want_terminal: bool = False, track_episodes: bool = True):
+                         want_terminal: bool = False, track_episodes: bool = True, outputs: dict | None = None):
         """A zero-argument callable that launches `rollout(actions, per_step_outputs=False)` on the
-        current stream: every C argument is converted once, here, so a launch costs one ctypes call
-        (for timed windows of a few tens of microseconds, where the Python checks and argument
-        conversion of `rollout` are a visible share of the host clock)."""
+        stream current at launch time with the sim's seed at launch time (a later reset(seed=...)
+        applies): every other C argument is converted once, here, so a launch costs one ctypes call
+        and two conversions (for timed windows of a few tens of microseconds, where the Python
+        checks and argument conversion of `rollout` are a visible share of the host clock)."""
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             raise ValueError("rollout_launcher: actions must be a contiguous float32 tensor on the sim's device")
         if actions.dim() != 3 or actions.shape[1:] != (self.n, 2) or actions.shape[0] < 1:
@@ -195,16 +206,31 @@ class BatchedAckermannSim:
         fn = _lib.lib().ackphys_rollout
         c = self._c
         flags = self.flags | (AUTORESET if autoreset else 0)
-        args = (self._ctx, C.c_int(int(actions.shape[0])), C.c_void_p(actions.data_ptr()), c["state"], c["obs_soa"],
-                c["reward"], c["term"], c["trunc"], c["terminal_obs_soa"] if (autoreset and want_terminal) else None,
-                c["info"] if want_info else None, c["episode"] if track_episodes else None, C.c_uint32(flags),
-                C.c_uint64(self.seed), C.c_int(0), C.c_void_p(_raw_stream(self._dev_index)))
+        k = int(actions.shape[0])
+        term_on = autoreset and want_terminal
+        if outputs is None:  # step K-1's outputs in the sim's own buffers (in place, as K step calls)
+            outs = (c["obs_soa"], c["reward"], c["term"], c["trunc"], c["terminal_obs_soa"] if term_on else None,
+                    c["info"] if want_info else None)
+        else:  # every step's outputs in its own slice of the caller's [K, ...] buffers (rollout_buffers)
+            shapes = {"obs": (k, NOBS, self.n), "reward": (k, self.n), "term": (k, self.n), "trunc": (k, self.n),
+                      "terminal_obs": (k, NOBS, self.n), "info": (k, 4, self.n)}
+            for name in ("obs", "reward", "term", "trunc") + (("terminal_obs",) if term_on else ()) + (
+                    ("info",) if want_info else ()):
+                t = outputs.get(name)
+                if t is None or tuple(t.shape) != shapes[name] or not t.is_contiguous() or t.device != self.device:
+                    raise ValueError(f"rollout_launcher: outputs[{name!r}] must be a contiguous {shapes[name]} tensor")
+            outs = (_ptr(outputs["obs"]), _ptr(outputs["reward"]), _ptr(outputs["term"]), _ptr(outputs["trunc"]),
+                    _ptr(outputs["terminal_obs"]) if term_on else None, _ptr(outputs["info"]) if want_info else None)
+        args = (self._ctx, C.c_int(k), C.c_void_p(actions.data_ptr()), c["state"], *outs,
+                c["episode"] if track_episodes else None, C.c_uint32(flags))
+        per_step, dev = C.c_int(0 if outputs is None else 1), self._dev_index
 
         def launch():
-            rc = fn(*args)
+            rc = fn(*args, self.seed, per_step, _raw_stream(dev))
             if rc:
                 _lib.check(rc, "ackphys_rollout")
-        launch.actions = actions  # keeps the action buffer alive as long as the launcher
+        launch.actions = actions  # keeps the action buffer (and the output slices) alive as long as the launcher
+        launch.outputs = outputs
         return launch
 
     def random_actions(self, k_steps: int, seed: int = 0, step0: int = 0) -> torch.Tensor:

@@ -875,6 +875,12 @@ static int plane_convex(const or_ctx* c, const or_data* d, int g1, int g2, doubl
    not unique (face/edge parallel to the separating plane) average the candidates within 1 um. */
 #define OR_TIE 1e-6
 #define OR_KINK_TOL 5e-7
+/* the kink snap below is a deliberate departure from mj_collision (whose general convex collider
+   has no such rule): it exists because the kernel's f32 edge search is rounding-limited at the
+   kink. or_set_kink_snap(0) turns it off so tests can bound what the snap changes (normal, depth:
+   tests/test_obstacle_scene.py::test_kink_snap_changes_only_the_tie) */
+static int g_kink_snap = 1;
+void or_set_kink_snap(int on) { g_kink_snap = on != 0; }
 static void box_frame(const or_data* d, const apm_model_t* m, int g, double c[3], double A[3][3], double h[3]) {
   for (int k = 0; k < 3; k++) {
     c[k] = d->geom_xpos[g][k];
@@ -993,7 +999,7 @@ static void edge_family(const double cc[3], const double a[3], double r, double 
   double nk[3];
   cross3(nk, a, A[k]);
   double len = sqrt(dot3(nk, nk));
-  if (len >= 1e-6) {
+  if (g_kink_snap && len >= 1e-6) {
     double il = (dot3(nk, n_out) < 0 ? -1.0 : 1.0) / len;
     for (int t = 0; t < 3; t++) nk[t] *= il;
     if (cyl_box_sep(cc, a, r, h, bc, A, bh, nk, &sg) >= cyl_box_sep(cc, a, r, h, bc, A, bh, n_out, &sg) - OR_KINK_TOL)

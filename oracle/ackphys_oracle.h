@@ -29,6 +29,8 @@ void or_set_env_variant(or_ctx* ctx, int action_repeat, int nohit_clear);
  * box-lattice cells within goal_cells breadth-first cells of the spawn (include/ackphys.h);
  * -1 if the world has no such lattice */
 int or_set_goal_cells(or_ctx* ctx, int goal_cells);
+/* obstacle scene: the wheel-on-box-edge kink snap (on by default; off = the plain search) */
+void or_set_kink_snap(int on);
 
 /* ackphys_step on host buffers (flags: ACKPHYS_CONTACTS | ACKPHYS_AUTORESET | ACKPHYS_POSTSTEP_OBS).
  * terminal_obs, info, episode may be NULL. nthreads <= 0: OpenMP default. */

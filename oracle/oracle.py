@@ -54,6 +54,7 @@ def lib():
         L.or_set_env_params.argtypes = [P, i32, C.c_double, C.c_double, C.c_double, C.c_double]
         L.or_set_env_variant.argtypes = [P, i32, i32]
         L.or_set_goal_cells.argtypes = [P, i32]
+        L.or_set_kink_snap.argtypes = [i32]
         L.or_philox.argtypes = [P, P, P]
         L.or_model_struct_size.restype = i32
         L.or_observe_raw.argtypes = [P, P, P, P, P, P, P, P, P, P]

@@ -40,6 +40,13 @@ def test_reference_imports_resolve():
             pass
         s = compute_episode_stats([1.0, 3.0], [10, 20])
         assert s["mean_return"] == 2.0 and s["std_length"] == 5.0
+        import numpy as np
+        from rl.utils import create_action_mapping, normalize_observation
+        class Box:
+            low = np.array([-1.0, 0.0, 2.0]); high = np.array([1.0, 4.0, 2.0])
+        assert np.allclose(normalize_observation(np.array([0.0, 1.0, 5.0]), Box()), [0.5, 0.25, 3.0])
+        assert normalize_observation("x", object()) == "x"
+        assert create_action_mapping(None, 0.5, 2.0)(np.array([1.0, -0.5])) == (0.5, -1.0)
         print("ok")
     """)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr

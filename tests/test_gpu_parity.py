@@ -103,7 +103,9 @@ def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
         if check_obs:
             gobs = sim.obs_soa.cpu().numpy().T
             do = np.abs(gobs - oobs) / (1.0 + 0.1 * np.abs(oobs))
-            horizon = np.array([_horizon_rays_excused(gobs[e], oobs[e], do[e]) for e in range(sim.n)])
+            horizon = np.zeros(sim.n, dtype=bool)
+            for e in np.nonzero(do.max(axis=1) > TOL_OBS)[0]:  # only envs with an entry over tolerance
+                horizon[e] = _horizon_rays_excused(gobs[e], oobs[e], do[e])
             worst["excused_rays"] += int((ok & horizon).sum())
             okr = ok & ~horizon
             worst["obs"] = max(worst["obs"], do[okr].max(initial=0.0))
@@ -415,20 +417,47 @@ def test_ragged_env_count(blob, variant):
     teacher_forced(sim, fresh_oracle(blob), acts, steps, 3, seed)
 
 
-def test_variants_agree_at_4096():
-    """All kernel mappings step the same 4096 envs to the same state (f32 summation order only)."""
-    n, steps = 4096, 50
-    sims = {v: make_sim(n, seed=2, contacts=True, variant=v) for v in ("lane", "quad", "lane16")}
-    acts = sims["lane"].random_actions(steps, seed=2)
+def test_variants_agree_at_4096(blob):
+    """All kernel mappings step the same 4096 envs to the same state within the stated f32
+    tolerances (|dqpos| <= 1e-5, |dqvel| <= 1e-3; they differ in summation order only). An env-step
+    where two mappings disagree beyond them is excused only if BOTH results are valid answers to the
+    f64 oracle (within the tolerances, or reproduced by it from a state shifted <= 1e-6 m: a contact
+    activation boundary, see the module docstring); excused env-steps are counted and capped at 0.1 %."""
+    n, steps, seed = 4096, 50, 2
+    sims = {v: make_sim(n, seed=seed, contacts=True, variant=v) for v in ("lane", "quad", "lane16")}
+    acts = sims["lane"].random_actions(steps, seed=seed)
     for s in sims.values():
         s.reset()
+    o = fresh_oracle(blob)
+    excused, worst = 0, dict(qpos=0.0, qvel=0.0)
     for k in range(steps):
         start = sims["lane"].state.clone()
         for s in sims.values():
             s.state.copy_(start)
             s.step(acts[k])
         torch.cuda.synchronize()
-        ref = sims["lane"].state
+        ref = f64_state(sims["lane"].state)
+        before = None
         for v in ("quad", "lane16"):
-            d = (sims[v].state[:25] - ref[:25]).abs().max().item()
-            assert d < 5e-3, (k, v, d)   # boundary cases included; typical 1e-6
+            g = f64_state(sims[v].state)
+            dq = np.abs(g[:, :13] - ref[:, :13]).max(axis=1)
+            dv = np.abs(g[:, 13:25] - ref[:, 13:25]).max(axis=1)
+            ok = (dq <= TOL_QPOS) & (dv <= TOL_QVEL)
+            worst["qpos"] = max(worst["qpos"], dq[ok].max(initial=0.0))
+            worst["qvel"] = max(worst["qvel"], dv[ok].max(initial=0.0))
+            if ok.all():
+                continue
+            if before is None:
+                before = f64_state(start)
+            a_np = acts[k].cpu().numpy()
+            for e in np.nonzero(~ok)[0]:
+                for res in (g[e], ref[e]):
+                    s1 = before[e][None].copy()
+                    o.step(s1, a_np[e][None], flags=3, seed=seed)
+                    good = (np.abs(res[:13] - s1[0, :13]).max() <= TOL_QPOS and
+                            np.abs(res[13:25] - s1[0, 13:25]).max() <= TOL_QVEL)
+                    assert good or _boundary_excused(o, before[e], a_np[e], res, 3, seed), (
+                        f"step {k} env {e} {v}: |dqpos| {dq[e]:.3e} |dqvel| {dv[e]:.3e}, not an oracle answer")
+                excused += 1
+    print("variants_agree", worst, "excused", excused, "of", 2 * steps * n)
+    assert excused <= 1e-3 * 2 * steps * n, excused

@@ -320,38 +320,70 @@ def test_adv_moments_two_ranks_normalise_the_world_minibatch():
         np.testing.assert_allclose(got[m, 1], 1.0 / (u.std(ddof=1) + 1e-8), rtol=1e-6)
 
 
-def test_fused_epoch_matches_per_minibatch_calls():
-    """ackppo_epoch (one C call per epoch) and the per-minibatch grad/reduce/adam calls give
-    bit-identical parameters, Adam moments and loss statistics."""
+def test_train_paths_bit_identical():
+    """PPO.train is one ackppo_train call. Its single-rank sequence (no hook), the data-parallel
+    sequence over a one-rank native RCCL communicator (ackppo_rccl_allreduce: the world > 1 path with
+    real RCCL calls) and over the host-staged hook (the gloo rehearsals' path, a no-op at world 1)
+    give bit-identical parameters, Adam moments and loss statistics -- and so does the C-level
+    ackppo_epoch loop of the same epochs."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     out = []
-    for fused in (True, False):
+    for coll in (None, "rccl", "host"):
         venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
-        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01)
-        model.fused_epoch = fused
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01, collective=coll)
+        assert (model.collective is None) == (coll is None)
         model.learn(total_timesteps=2 * 16 * 256)
         out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
                     model.logger["train/value_loss"], model.logger["train/approx_kl"]))
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    assert out[0][2:] == out[1][2:]
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0][0], o[0])
+        np.testing.assert_array_equal(out[0][1], o[1])
+        assert out[0][2:] == o[2:]
+
+
+def test_train_matches_epoch_calls():
+    """ackppo_train (world 1, no hook) = per epoch ackppo_permutation + ackppo_adv_stats + ackppo_epoch."""
+    from mujoco_playground_amd.rl import make_ackermann_env
+    from mujoco_playground_amd.rl.ppo import PPO
+    venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
+    model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01)
+    model.collect_rollouts()
+    snap = [t.clone() for t in (model.params, model.exp_avg, model.exp_avg_sq)]
+    model.train()
+    got = [t.clone() for t in (model.params, model.exp_avg, model.exp_avg_sq, model.loss_acc)]
+    for t, v in zip((model.params, model.exp_avg, model.exp_avg_sq), snap):
+        t.copy_(v)
+    model.loss_acc.zero_()
+    n_idx, B = 16 * 256, 1000
+    nmb = (n_idx + B - 1) // B
+    step0 = model.adam_step - 3 * nmb
+    for ep in range(3):
+        assert L().ackppo_permutation(n_idx, model.perm_key, ep, P(model.perm), S()) == 0
+        assert L().ackppo_adv_stats(P(model.buf_adv), P(model.perm), n_idx, B, 1, P(model.mb_stats), S()) == 0
+        assert L().ackppo_epoch(P(model.params), P(model.buf_obs), P(model.buf_act), P(model.buf_logp),
+                                P(model.buf_adv), P(model.buf_ret), P(model.perm), n_idx, B, P(model.mb_stats), 0.2, 0.01,
+                                0.5, 0.5, 3e-4, 0.9, 0.999, 1e-5, step0 + ep * nmb, P(model.gpart), P(model.lpart),
+                                P(model.grad), P(model.loss_acc), P(model.exp_avg), P(model.exp_avg_sq),
+                                P(model.gnorm), S()) == 0
+    for a, b in zip(got, (model.params, model.exp_avg, model.exp_avg_sq, model.loss_acc)):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("variant", [{}, {"action_repeat": 5, "nohit_clear": True}])
 def test_obstacle_scene_ppo_4096(variant):
     """PPO on the obstacle scene at the bench's per-GPU shape (4096 envs; the fused rollout in the obst8
-    kernel), the fused epoch and the per-minibatch calls (the data-parallel path's kernels) bit-equal,
-    with the reference task and with the opt-in learnable variant."""
+    kernel), the single-rank update and the data-parallel one over a one-rank RCCL communicator
+    bit-equal, with the reference task and with the opt-in learnable variant."""
     from mujoco_playground_amd.rl import AckermannVecEnv
     from mujoco_playground_amd.rl.ppo import PPO
     out = []
-    for fused in (True, False):
+    for coll in (None, "rccl"):
         venv = AckermannVecEnv(4096, device=DEV, seed=4, contacts=True, scene="obstacles", max_episode_steps=24,
                                **variant)
-        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=8192, n_epochs=2, seed=5, ent_coef=0.01)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=8192, n_epochs=2, seed=5, ent_coef=0.01,
+                    collective=coll)
         assert model.fused_rollout
-        model.fused_epoch = fused
         model.learn(total_timesteps=3 * 16 * 4096)
         assert torch.isfinite(model.params).all()
         lg = model.logger

@@ -231,3 +231,27 @@ def test_edge_family_kink_witness():
     centre = xpos[b] + xmat[b] @ m.geom_pos[g]
     assert abs(a @ n) < 1e-9
     assert abs(a @ (box[0, 3:6] - centre)) < 1e-9   # mid-plane witness
+
+
+def test_kink_snap_is_a_no_op_in_f64():
+    """The kink snap (oracle edge_family / kernel cb_edge_family) is a deliberate departure from
+    mj_collision: MuJoCo's general convex collider has no such rule; it exists because the kernel's
+    f32 edge search is rounding-limited at the kink (|dqvel| 0.18 on the recorded state before it).
+    It must not change the oracle's own f64 answer: with the snap off, the f64 search gives the same
+    contacts (pairs, depth, normal, point) on the recorded state to 1e-9, so the rule cannot hide a
+    discrepancy of the f64 restatement -- it only pulls the f32 kernel onto the answer the f64 search
+    finds by itself."""
+    import os
+    from mujoco_playground_amd import _lib
+    from oracle.oracle import Oracle, lib
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "edge_kink_state.npz"))
+    o = Oracle(_lib.load_blob("obstacles"))
+    on = o.contacts(d["before"][:13])
+    lib().or_set_kink_snap(0)
+    try:
+        off = o.contacts(d["before"][:13])
+    finally:
+        lib().or_set_kink_snap(1)
+    assert on.shape == off.shape and ((on[:, 0] >= 41) & (on[:, 1] < 41)).sum() == 1   # the wheel-box contact
+    np.testing.assert_array_equal(on[:, :2], off[:, :2])
+    np.testing.assert_allclose(on[:, 2:15], off[:, 2:15], rtol=0, atol=1e-9)

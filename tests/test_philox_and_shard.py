@@ -46,7 +46,21 @@ def _worker(rank, world, port, q):
     shard.all_reduce_sum_(grad, w)
     params = torch.full((3,), float(10 * r + 7))
     shard.broadcast_(params, w)
-    q.put((r, shard.env_offset(r, n), tuple(g.shape), s, m, grad.tolist(), params.tolist()))
+    # the trainer's host-staged all-reduce hook (gloo rehearsals), called through its C function
+    # pointer as ackppo_train calls it: f32 gradient and f64 moments buffers, SUM in place
+    import ctypes as C
+    from mujoco_playground_amd import _lib
+    coll = shard.TrainerCollective(w, torch.device("cpu"))
+    assert coll.kind == "host"
+    g32 = torch.full((6,), float(r + 1))
+    m64 = torch.full((4,), 0.5 * (r + 1), dtype=torch.float64)
+    coll.register(g32)
+    coll.register(m64)
+    fn = _lib.ALLREDUCE_FN(coll.fn.value)
+    rc = (fn(g32.data_ptr(), 6, 0, None, None), fn(m64.data_ptr(), 4, 1, None, None),
+          fn(g32.data_ptr(), 5, 0, None, None))   # an unregistered (ptr, count): reported, not a crash
+    q.put((r, shard.env_offset(r, n), tuple(g.shape), s, m, grad.tolist(), params.tolist(),
+           (rc, g32.tolist(), m64.tolist())))
     dist.destroy_process_group()
 
 
@@ -60,7 +74,8 @@ def test_sharded_gather_gloo_world2():
     res = sorted(q.get(timeout=120) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    (r0, off0, sh0, s0, m0, g0, p0), (r1, off1, sh1, s1, m1, g1, p1) = res
+    (r0, off0, sh0, s0, m0, g0, p0, h0), (r1, off1, sh1, s1, m1, g1, p1, h1) = res
+    assert h0 == h1 == ((0, 0, -1), [3.0] * 6, [1.5] * 4)   # the hook's SUMs; -1 for the unknown buffer
     assert g0 == g1 == [3.0] * 5          # 1 + 2 summed over ranks
     assert p0 == p1 == [7.0] * 3          # rank 0's parameters everywhere
     assert (off0, off1) == (0, 8)

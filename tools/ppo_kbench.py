@@ -82,14 +82,15 @@ def stamps(path):
     L.ackppo_grad_blocks.argtypes = [C.c_int]
     nblk = L.ackppo_grad_blocks(B)
     gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
-    st = torch.zeros(16 * nblk, dtype=torch.int64, device=dev)
+    st = torch.zeros(16 * 2 * nblk, dtype=torch.int64, device=dev)  # grad1: two workgroups per row
     L.ackppo_diag_set_stamps(P(st))
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(3):
         L.ackppo_grad(P(params), P(obs), P(act), P(lp), P(adv), P(ret), P(idx), B, P(stats), 0.2, 0.0, 0.5, P(gp),
                       P(lpart), s)
     torch.cuda.synchronize()
-    a = st.cpu().numpy().reshape(16, nblk)
+    a = st.cpu().numpy().reshape(16, -1)
+    a = a[:, : int((a[0] != 0).sum())]
     used = [k for k in range(16) if a[k].any()]
     print("grad phases (median cycles per workgroup):",
           {f"{used[i]}->{used[i + 1]}": int(np.median(a[used[i + 1]] - a[used[i]])) for i in range(len(used) - 1)},

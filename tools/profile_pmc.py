@@ -11,7 +11,9 @@ timed launch (the kernel's last dispatch) are divided by its K steps: bytes and 
 step. Entries are keyed "<kernel>@K<k>"; bench.py reports the entry whose K equals its --steps (or
 the nearest K, saying so), since a launch's first-step loads and last-step stores are spread over
 its K steps.
-    python3 tools/profile_pmc.py [K,K,...]     (default 20,1000: the driver's and bench's defaults)
+    python3 tools/profile_pmc.py [K,K,...] [--buffers]   (default 20,1000: the driver's and bench's defaults)
+--buffers: the same launches with per-step output slices (bench.py --buffers: a [K][79][N] rollout
+buffer), keyed "<kernel>@K<k>+buf" with per_step_outputs true.
 """
 import csv
 import glob
@@ -22,14 +24,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {0: "ackphys_rollout_nc_kernel", 1: "ackphys_rollout_quad_kernel"}
-KS = [int(k) for k in (sys.argv[1] if len(sys.argv) > 1 else "20,1000").split(",")]
+ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+BUFFERS = "--buffers" in sys.argv[1:]
+KS = [int(k) for k in (ARGS[0] if ARGS else "20,1000").split(",")]
 
 
 def run_pass(counters, out, contacts, k):
     os.makedirs(out, exist_ok=True)
     cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
            "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
-           "--no-obstacles", "--no-per-step", "--steps", str(k), "--warmup", "5", "--contacts", str(contacts)]
+           "--no-obstacles", "--no-per-step", "--no-buffer-leg", "--steps", str(k), "--warmup", "5", "--contacts",
+           str(contacts)] + (["--buffers"] if BUFFERS else [])
     env = dict(os.environ, TMPDIR="/tmp")
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, stdout=subprocess.DEVNULL)
     vals = {c: {} for c in counters}  # counter -> dispatch id -> value (summed over the rows of a dispatch)
@@ -46,13 +51,14 @@ def main():
     res = {}
     for k in KS:
         for contacts, kern in KERNELS.items():
-            out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}_k{k}")
+            out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}_k{k}{'_buf' if BUFFERS else ''}")
             f = run_pass(["FETCH_SIZE"], out + "_fetch", contacts, k)["FETCH_SIZE"]
             w = run_pass(["WRITE_SIZE"], out + "_write", contacts, k)["WRITE_SIZE"]
             sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts, k)
             ok = f is not None and w is not None
-            res[f"{kern}@K{k}"] = {
-                "kernel": kern, "contacts": bool(contacts), "launch_steps": k, "FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w,
+            key = f"{kern}@K{k}" + ("+buf" if BUFFERS else "")
+            res[key] = {
+                "kernel": kern, "contacts": bool(contacts), "launch_steps": k, "per_step_outputs": BUFFERS, "FETCH_SIZE_kB": f, "WRITE_SIZE_kB": w,
                 "hbm_bytes_per_launch": (2 * f * 1024 + w * 1024) if ok else None,
                 "hbm_bytes_per_step": (2 * f * 1024 + w * 1024) / k if ok else None,
                 "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B), WRITE_SIZE as reported",
@@ -60,8 +66,9 @@ def main():
                 "SQ_INSTS_VALU": sq["SQ_INSTS_VALU"], "SQ_INSTS_SALU": sq["SQ_INSTS_SALU"], "SQ_WAVES": sq["SQ_WAVES"],
                 "valu_insts_per_wave_step": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] / k) if sq["SQ_WAVES"] else None,
             }
-            print(json.dumps({f"{kern}@K{k}": res[f"{kern}@K{k}"]}), flush=True)
-    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest.json"), "w"), indent=1)
+            print(json.dumps({key: res[key]}), flush=True)
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest" + ("_buf" if BUFFERS else "") + ".json"), "w"),
+              indent=1)
 
 
 if __name__ == "__main__":
