@@ -203,6 +203,18 @@ typedef struct {
   int world;
   ackppo_allreduce_fn allreduce;
   void* allreduce_user;
+  /* nullable [NPARAM] scratch, zero-filled once by the caller (never written outside the layout's
+   * parameters): with all three, each minibatch's Adam step is applied by the NEXT minibatch's
+   * gradient launch while it stages the weights (same arithmetic and bits as ackppo_adam, one
+   * launch less per minibatch), the parameter / moment vectors alternating between the caller's and
+   * these; the result ends in the caller's vectors */
+  float* params2;
+  float* exp_avg2;
+  float* exp_avg_sq2;
+  /* opt-in entropy floor (not an SB3 parameter; -INFINITY = SB3, bit for bit): log_std is held at or
+   * above this value after every Adam step, so the DiagGaussian's spread cannot collapse below
+   * exp(log_std_min) */
+  float log_std_min;
 } ackppo_train_desc;
 
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch

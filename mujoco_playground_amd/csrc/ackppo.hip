@@ -43,9 +43,19 @@ __device__ unsigned long long* g_pp_stamps;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");               \
     if (threadIdx.x == 0) g_pp_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;                 \
   } while (0)
+// the 100 MHz constant clock (workgroup start / end across the grid: the kernel's timeline)
+#define PRSTAMP(k)                                                                             \
+  do {                                                                                         \
+    unsigned long long _t;                                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
+    if (threadIdx.x == 0) g_pp_stamps[(size_t)(k)*gridDim.x + blockIdx.x] = _t;                 \
+  } while (0)
 #else
 #define PSTAMP(k) \
   do {            \
+  } while (0)
+#define PRSTAMP(k) \
+  do {             \
   } while (0)
 #endif
 
@@ -61,11 +71,20 @@ constexpr Net CRITIC{ACKPPO_OFF_VF_W1, ACKPPO_OFF_VF_B1, ACKPPO_OFF_VF_W2, ACKPP
 using ppm::fexp;
 using ppm::ftanh;
 using ppm::gauss_term;
+using ppm::f4v;   // f32 MFMA 16x16x4 (exact f32 products, a k-ordered fmaf chain; ackppo_math.inc)
+using ppm::mfma4;
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+// LDS written by some lanes of this wave, read by others: order the accesses (one wave's LDS
+// operations execute in order) and keep the compiler from moving them across
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace pp
@@ -237,13 +256,65 @@ struct GradArgs {
   float clip, ent_coef, vf_coef;
   float* gpart;
   float* lpart;
+  // the previous minibatch's Adam step, applied while staging (ackppo_train; upd == nullptr: none):
+  // params (above) / m_in / v_in and the reduced gradient upd -> p_out / m_out / v_out (every
+  // workgroup computes its net's new values; the one with tile (index mod rows) == its row writes them)
+  const float* upd;
+  const float* m_in;
+  const float* v_in;
+  float* p_out;
+  float* m_out;
+  float* v_out;
+  float scale, max_norm, b1, b2, eps, step_size, bc2_sqrt;
+  float* norm_out;
+  float lsmin;  // opt-in log_std floor (ackppo_train_desc::log_std_min; -inf: none)
 };
 
-// ---- ackppo_grad LDS map (floats). Weights: staged once per workgroup, the first layers
-// transposed ([k][unit], so a lane's 16 units are 4 contiguous 16-B reads), the second layers
-// row-major. Tile: GT samples, rows of GLDP floats (16-B aligned): X [80 rows], per net
-// h1, h2, d2, d1 [64 rows each], then gmu [2], glog [2], gv [1] rows.
-constexpr int GT = 32, GLDP = 36;
+// ---- Adam (torch.optim.Adam after clip_grad_norm_), shared by ackppo_adam_kernel and the update
+// fused into ackppo_grad1_kernel's staging so both give the same bits: the global norm of
+// scale * grad summed in one fixed order by every 256-thread workgroup (thread t: float4 j = t + 256 k
+// ascending, x^2 + y^2 + z^2 + w^2 each; wave shuffles; the four wave sums in order), then the
+// per-parameter update.
+struct AdamK {
+  float scale, coef, b1, b2, eps, step_size, bc2_sqrt, lsmin;
+};
+__device__ __forceinline__ float grad_norm256(const float* __restrict__ g, float scale, float* red) {
+  static_assert(P % 4 == 0, "float4 parameter vector");
+  const int tid = threadIdx.x;
+  float ss = 0.0f;
+  for (int j = tid; j < P / 4; j += 256) {
+    const float4 v = reinterpret_cast<const float4*>(g)[j];
+    const float x = v.x * scale, y = v.y * scale, z = v.z * scale, w = v.w * scale;
+    ss = fmaf(x, x, ss);
+    ss = fmaf(y, y, ss);
+    ss = fmaf(z, z, ss);
+    ss = fmaf(w, w, ss);
+  }
+  ss = wave_sum(ss);
+  __syncthreads();  // red may be in use
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  return sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+}
+__device__ __forceinline__ AdamK adam_k(float norm, float scale, float max_norm, float b1, float b2, float eps,
+                                        float step_size, float bc2_sqrt, float lsmin) {
+  return AdamK{scale, fminf(max_norm / (norm + 1e-6f), 1.0f), b1, b2, eps, step_size, bc2_sqrt, lsmin};  // clip_grad_norm_
+}
+// the opt-in entropy floor: log_std held at or above lsmin after its Adam step (-inf: untouched, bit for bit)
+__device__ __forceinline__ float ls_floor(const AdamK& k, float ls) { return k.lsmin > -INFINITY ? fmaxf(ls, k.lsmin) : ls; }
+__device__ __forceinline__ void adam_elem(const AdamK& k, float p, float g, float m, float v, float& pn, float& mn,
+                                          float& vn) {
+  // no fma contraction: the fused (staging) and unfused (ackppo_adam_kernel) instances must round
+  // alike wherever the compiler inlines them
+#pragma clang fp contract(off)
+  const float gi = g * k.scale * k.coef;
+  mn = m + (1.0f - k.b1) * (gi - m);                 // exp_avg.lerp_(grad, 1 - beta1)
+  vn = v * k.b2 + (1.0f - k.b2) * gi * gi;           // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  pn = p - k.step_size * (mn / (sqrtf(vn) / k.bc2_sqrt + k.eps));
+}
+
+// ---- staged policy weights (ackppo_act's LDS map, floats): the first layers transposed ([k][unit],
+// so a lane's 16 units are 4 contiguous 16-B reads), the second layers row-major.
 // W1T: [80][128] = [k][actor|critic unit], W2: [unit][k] row-major per net. Both are XOR-swizzled
 // (w1t_at / w2_at) so the MFMA operand reads -- 16 consecutive units x 4 consecutive k per wave --
 // hit 64 distinct LDS banks (W1T, layer-2 W2 reads) or at most 4 lanes per bank (W2^T reads).
@@ -258,14 +329,8 @@ __device__ __forceinline__ int w2_at(int u, int k) { return u * H + (k ^ (4 * (u
 constexpr int W_B1_A = W_W2_C + H * H, W_B2_A = W_B1_A + H, W_B1_C = W_B2_A + H, W_B2_C = W_B1_C + H;
 constexpr int W_AW = W_B2_C + H, W_AB = W_AW + 2 * H, W_CW = W_AB + 4, W_CB = W_CW + H, W_LS = W_CB + 4;
 constexpr int W_TOTAL = W_LS + 4;
-constexpr int G_X = W_TOTAL, G_NET = G_X + 80 * GLDP, G_NETSZ = 4 * H * GLDP;
-constexpr int G_H1 = 0, G_H2 = H * GLDP, G_D2 = 2 * H * GLDP, G_D1 = 3 * H * GLDP;
-constexpr int G_VEC = G_NET + 2 * G_NETSZ;
-constexpr int G_GMU = G_VEC, G_GLOG = G_VEC + 2 * GLDP, G_GV = G_VEC + 4 * GLDP;
-constexpr int G_TOTAL = G_VEC + 5 * GLDP;
-static_assert(G_TOTAL * 4 <= 160 * 1024, "grad workgroup exceeds the 160 KiB LDS of a CU");
 constexpr int GRAD_THREADS = 256;
-constexpr int GRAD_MAX_BLOCKS = 256;  // one workgroup per CU (the LDS footprint allows one)
+constexpr int GRAD_MAX_BLOCKS = 256;  // partial gradient rows (one per 32-sample tile) at most
 
 __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, float* w) {
   // Every global load of the staging is issued before the first LDS write (W1, W2 as 16-B loads,
@@ -332,395 +397,13 @@ __device__ __forceinline__ void stage_grad_weights(const float* __restrict__ p, 
   if (has_sc) w[sc < 2 ? W_AB + sc : (sc < 4 ? W_LS + sc - 2 : W_CB)] = vsc;
 }
 
-__device__ __forceinline__ float row_sum_g(const float* a) {
-  float s = 0.0f;
-#pragma unroll
-  for (int i = 0; i < GT; i += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(a + i);
-    s += (v.x + v.y) + (v.z + v.w);
-  }
-  return s;
-}
-__device__ __forceinline__ float row_dot_g(const float* a, const float* b) {
-  float s = 0.0f;
-#pragma unroll
-  for (int i = 0; i < GT; i += 4) {
-    const float4 u = *reinterpret_cast<const float4*>(a + i), v = *reinterpret_cast<const float4*>(b + i);
-    s = fmaf(u.x, v.x, s);
-    s = fmaf(u.y, v.y, s);
-    s = fmaf(u.z, v.z, s);
-    s = fmaf(u.w, v.w, s);
-  }
-  return s;
-}
-
-// vector gradient entries (biases, heads, log_std: 453; see vec_item), PERV per thread
-constexpr int NVEC = 453;
-constexpr int PERV = (NVEC + GRAD_THREADS - 1) / GRAD_THREADS;
-
-// f32 MFMA 16x16x4 (exact f32 products, k-ordered fmaf chain): lane l supplies A[l & 15][l >> 4]
-// and B[l >> 4][l & 15]; D[row 4 (l >> 4) + r][col l & 15] comes back in element r.
-using ppm::f4v;
-using ppm::mfma4;
-
-__device__ __forceinline__ float vec_item(const float* tl, int i) {
-  const float* an = tl + G_NET;
-  const float* cn = tl + G_NET + G_NETSZ;
-  if (i < 64) return row_sum_g(an + G_D1 + i * GLDP);
-  if (i < 128) return row_sum_g(an + G_D2 + (i - 64) * GLDP);
-  if (i < 192) return row_sum_g(cn + G_D1 + (i - 128) * GLDP);
-  if (i < 256) return row_sum_g(cn + G_D2 + (i - 192) * GLDP);
-  if (i < 384) {
-    const int d = (i - 256) >> 6, j = (i - 256) & 63;
-    return row_dot_g(tl + G_GMU + d * GLDP, an + G_H2 + j * GLDP);
-  }
-  if (i < 386) return row_sum_g(tl + G_GMU + (i - 384) * GLDP);
-  if (i < 450) return row_dot_g(tl + G_GV, cn + G_H2 + (i - 386) * GLDP);
-  if (i == 450) return row_sum_g(tl + G_GV);
-  return row_sum_g(tl + G_GLOG + (i - 451) * GLDP);
-}
-__device__ __forceinline__ int vec_offset(int i) {
-  if (i < 64) return ACKPPO_OFF_PI_B1 + i;
-  if (i < 128) return ACKPPO_OFF_PI_B2 + i - 64;
-  if (i < 192) return ACKPPO_OFF_VF_B1 + i - 128;
-  if (i < 256) return ACKPPO_OFF_VF_B2 + i - 192;
-  if (i < 384) return ACKPPO_OFF_ACT_W + (i - 256);
-  if (i < 386) return ACKPPO_OFF_ACT_B + i - 384;
-  if (i < 450) return ACKPPO_OFF_VAL_W + i - 386;
-  if (i == 450) return ACKPPO_OFF_VAL_B;
-  return ACKPPO_OFF_LOG_STD + i - 451;
-}
-
-// One workgroup per CU; workgroup b processes tiles b, b + grid, ... of GT samples and keeps its
-// weight gradients in registers across tiles, writing one partial row at the end.
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_grad_kernel(GradArgs A) {
-  PSTAMP(0);
-  extern __shared__ float tl[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s = lane & 31, uh = lane >> 5;            // per-sample phases: sample in tile, lane half
-  const int nid = wave >> 1;                          // 0 actor, 1 critic
-  float* w = tl;
-  float* nt = tl + G_NET + nid * G_NETSZ;
-  const float invB = 1.0f / (float)A.batch;
-  const int ntiles = (A.batch + GT - 1) / GT;
-  // gather of a tile's observation rows: thread t holds 10 words of row (t >> 3). The first
-  // tile's loads are issued before the weight staging, so their latency hides under it.
-  float xg[10];
-  auto gather_load = [&](int tile) __attribute__((always_inline)) {
-    const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
-    const int r = tid >> 3, q = tid & 7;
-    const bool ok = r < nvalid;
-    const float* row = A.obs_rows + (size_t)(ok ? A.idx[s0 + r] : 0) * NOBS;
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-      const int k = q * 10 + i;
-      xg[i] = (ok && k < NOBS) ? row[k] : 0.0f;
-    }
-  };
-  // the heads' per-sample inputs (actor lanes: action, old log-prob, advantage; critic lanes:
-  // return), loaded with the gather for the same reason
-  const bool head_lane = uh == 0 && (wave & 1) == 0;
-  float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto head_load = [&](int tile) __attribute__((always_inline)) {
-    const int s0 = tile * GT;
-    if (head_lane && s < min(GT, A.batch - s0)) {
-      const int sidx = A.idx[s0 + s];
-      if (nid == 0) {
-        hin[0] = A.actions[2 * (size_t)sidx];
-        hin[1] = A.actions[2 * (size_t)sidx + 1];
-        hin[2] = A.old_logp[sidx];
-        hin[3] = A.adv[sidx];
-      } else {
-        hin[0] = A.ret[sidx];
-      }
-    }
-  };
-  if (blockIdx.x < ntiles) {
-    gather_load(blockIdx.x);
-    head_load(blockIdx.x);
-  }
-  stage_grad_weights(A.params, w);
-
-  // MFMA tiles: lane (li, lk) = (lane & 15, lane >> 4). Wave w owns unit tiles ut = 2w, 2w + 1
-  // of the 128 actor|critic units (16 each; its net is w >> 1, its units within the net
-  // 32 (w & 1) + 16 t + ...) in every GEMM below. Weight gradients stay in the accumulators
-  // across tiles: gW1 [2 unit tiles][5 k tiles of the 80 inputs], gW2 [2][4 k tiles of 64].
-  const int li = lane & 15, lk = lane >> 4;
-  const int ub0 = 32 * (wave & 1);  // first unit (within the wave's net) of the wave's two tiles
-  f4v gw1[2][5], gw2[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) gw1[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < 4; j++) gw2[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-  }
-  float accv[PERV];
-#pragma unroll
-  for (int b = 0; b < PERV; b++) accv[b] = 0.0f;
-  float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int s0 = tile * GT, nvalid = min(GT, A.batch - s0);
-    __syncthreads();  // previous tile's LDS reads are done (and the weights are staged)
-    if (tile != blockIdx.x) {
-      gather_load(tile);
-      head_load(tile);
-    }
-    {
-      const int r = tid >> 3, q = tid & 7;
-#pragma unroll
-      for (int i = 0; i < 10; i++) tl[G_X + (q * 10 + i) * GLDP + r] = xg[i];
-    }
-    __syncthreads();
-    PSTAMP(1);
-    const bool valid = s < nvalid;
-    // GEMM-shaped layers: thread (ub, sb) owns 4 units (of the 128 actor|critic units) x 4 samples
-    const int ub = tid >> 3, sb = tid & 7, gnet = ub >> 4, gu = 4 * (ub & 15), gs = 4 * sb;
-    float* gt = tl + G_NET + gnet * G_NETSZ;  // this thread's net tile
-    {  // layer 1: H1 = tanh(W1 X + b1): [128 units x 32 samples] = W1T^T [128 x 80] . X [80 x 32]
-      f4v acc[2][2];
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll  // k0 compile-time: the W1T swizzle folds to an immediate XOR per read
-      for (int k0 = 0; k0 < 80; k0 += 4) {
-        const int k = k0 + lk;
-        const float a0 = w[w1t_at(k, nid * H + ub0 + li)], a1 = w[w1t_at(k, nid * H + ub0 + 16 + li)];
-        const float b0 = tl[G_X + k * GLDP + li], b1 = tl[G_X + k * GLDP + 16 + li];
-        acc[0][0] = mfma4(a0, b0, acc[0][0]);
-        acc[0][1] = mfma4(a0, b1, acc[0][1]);
-        acc[1][0] = mfma4(a1, b0, acc[1][0]);
-        acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      }
-      const float* bias = w + (nid ? W_B1_C : W_B1_A);
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = ub0 + 16 * t + 4 * lk + r;
-          const float bb = bias[u];
-#pragma unroll
-          for (int j = 0; j < 2; j++) nt[G_H1 + u * GLDP + 16 * j + li] = ftanh(acc[t][j][r] + bb);
-        }
-    }
-    __syncthreads();
-    PSTAMP(2);
-    {  // layer 2: H2 = tanh(W2 H1 + b2) per net: [64 x 32] = W2 [64 x 64] . H1 [64 x 32]
-      const float* W2 = w + (nid ? W_W2_C : W_W2_A);
-      f4v acc[2][2];
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;
-        const float a0 = W2[w2_at(ub0 + li, k)], a1 = W2[w2_at(ub0 + 16 + li, k)];
-        const float b0 = nt[G_H1 + k * GLDP + li], b1 = nt[G_H1 + k * GLDP + 16 + li];
-        acc[0][0] = mfma4(a0, b0, acc[0][0]);
-        acc[0][1] = mfma4(a0, b1, acc[0][1]);
-        acc[1][0] = mfma4(a1, b0, acc[1][0]);
-        acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      }
-      const float* bias = w + (nid ? W_B2_C : W_B2_A);
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = ub0 + 16 * t + 4 * lk + r;
-          const float bb = bias[u];
-#pragma unroll
-          for (int j = 0; j < 2; j++) nt[G_H2 + u * GLDP + 16 * j + li] = ftanh(acc[t][j][r] + bb);
-        }
-    }
-    __syncthreads();
-    PSTAMP(3);
-    if (uh == 0 && (wave & 1) == 0) {  // heads + loss gradient: 32 lanes of waves 0 (actor) and 2 (critic)
-      float h[H];
-#pragma unroll
-      for (int k = 0; k < H; k++) h[k] = nt[G_H2 + k * GLDP + s];
-      if (nid == 0) {
-        float mu[NA], a[NA];
-#pragma unroll
-        for (int d = 0; d < NA; d++) {
-          float m = 0.0f;
-#pragma unroll
-          for (int j = 0; j < H; j++) m = fmaf(w[W_AW + d * H + j], h[j], m);
-          mu[d] = m + w[W_AB + d];
-        }
-        a[0] = hin[0];
-        a[1] = hin[1];
-        float logp = 0.0f;
-#pragma unroll
-        for (int d = 0; d < NA; d++) logp += gauss_term(a[d], mu[d], w[W_LS + d]);
-        const float lr = logp - hin[2];
-        const float r = fexp(lr);
-        const float adv = (hin[3] - A.stats[0]) * A.stats[1];
-        const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
-        const float l1 = adv * r, l2 = adv * rc;
-        // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
-        // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
-        const float glogp = valid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
-#pragma unroll
-        for (int d = 0; d < NA; d++) {
-          const float inv_var = fexp(-2.0f * w[W_LS + d]);
-          const float dv = a[d] - mu[d];
-          tl[G_GMU + d * GLDP + s] = glogp * dv * inv_var;
-          tl[G_GLOG + d * GLDP + s] = glogp * (dv * dv * inv_var - 1.0f);
-        }
-        if (valid) {
-          la += -fminf(l1, l2);
-          lb += (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
-          lc += (r - 1.0f) - lr;
-          ln += 1.0f;
-        }
-      } else {
-        float v = 0.0f;
-#pragma unroll
-        for (int j = 0; j < H; j++) v = fmaf(w[W_CW + j], h[j], v);
-        v += w[W_CB];
-        const float R = hin[0];
-        tl[G_GV + s] = valid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
-        if (valid) la += (R - v) * (R - v);
-      }
-    }
-    __syncthreads();
-    PSTAMP(4);
-    {  // d2 = (dL/dh2) (1 - h2^2) for this thread's 4 units x 4 samples
-      const float4 hv0 = *reinterpret_cast<const float4*>(tl + G_GMU + gs);
-      const float4 hv1 = *reinterpret_cast<const float4*>(tl + G_GMU + GLDP + gs);
-      const float4 gvv = *reinterpret_cast<const float4*>(tl + G_GV + gs);
-      const float g0[4] = {hv0.x, hv0.y, hv0.z, hv0.w}, g1[4] = {hv1.x, hv1.y, hv1.z, hv1.w};
-      const float gv[4] = {gvv.x, gvv.y, gvv.z, gvv.w};
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int u = gu + i;
-        const float4 h2 = *reinterpret_cast<const float4*>(gt + G_H2 + u * GLDP + gs);
-        const float ha[4] = {h2.x, h2.y, h2.z, h2.w};
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const float dh = gnet == 0 ? g0[j] * w[W_AW + u] + g1[j] * w[W_AW + H + u] : gv[j] * w[W_CW + u];
-          o[j] = dh * (1.0f - ha[j] * ha[j]);
-        }
-        *reinterpret_cast<float4*>(gt + G_D2 + u * GLDP + gs) = make_float4(o[0], o[1], o[2], o[3]);
-      }
-    }
-    __syncthreads();
-    PSTAMP(5);
-    {  // d1 = (W2^T d2) (1 - h1^2): [64 x 32] = W2^T [64 x 64] . D2 [64 x 32] per net
-      const float* W2 = w + (nid ? W_W2_C : W_W2_A);
-      f4v acc[2][2];
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[t][j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;  // layer-2 unit
-        const float a0 = W2[w2_at(k, ub0 + li)], a1 = W2[w2_at(k, ub0 + 16 + li)];
-        const float b0 = nt[G_D2 + k * GLDP + li], b1 = nt[G_D2 + k * GLDP + 16 + li];
-        acc[0][0] = mfma4(a0, b0, acc[0][0]);
-        acc[0][1] = mfma4(a0, b1, acc[0][1]);
-        acc[1][0] = mfma4(a1, b0, acc[1][0]);
-        acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      }
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = ub0 + 16 * t + 4 * lk + r;
-#pragma unroll
-          for (int j = 0; j < 2; j++) {
-            const float h1 = nt[G_H1 + u * GLDP + 16 * j + li];
-            nt[G_D1 + u * GLDP + 16 * j + li] = acc[t][j][r] * (1.0f - h1 * h1);
-          }
-        }
-    }
-    __syncthreads();
-    PSTAMP(6);
-    // weight-gradient sums over the tile's samples (rows of padding samples are zero):
-    // gW1 [units x 80] += D1 [units x 32] . X^T [32 x 80], gW2 [units x 64] += D2 . H1^T
-#pragma unroll
-    for (int q0 = 0; q0 < GT; q0 += 4) {
-      const int q = q0 + lk;  // sample
-      const float a0 = nt[G_D1 + (ub0 + li) * GLDP + q], a1 = nt[G_D1 + (ub0 + 16 + li) * GLDP + q];
-      const float c0 = nt[G_D2 + (ub0 + li) * GLDP + q], c1 = nt[G_D2 + (ub0 + 16 + li) * GLDP + q];
-#pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const float bx = tl[G_X + (16 * j + li) * GLDP + q];
-        gw1[0][j] = mfma4(a0, bx, gw1[0][j]);
-        gw1[1][j] = mfma4(a1, bx, gw1[1][j]);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const float bh = nt[G_H1 + (16 * j + li) * GLDP + q];
-        gw2[0][j] = mfma4(c0, bh, gw2[0][j]);
-        gw2[1][j] = mfma4(c1, bh, gw2[1][j]);
-      }
-    }
-#pragma unroll
-    for (int bb = 0; bb < PERV; bb++) {
-      const int i = tid + bb * GRAD_THREADS;
-      if (i < NVEC) accv[bb] += vec_item(tl, i);
-    }
-  }
-  PSTAMP(7);
-  // this workgroup's partial gradient row and loss sums
-  float* g = A.gpart + (size_t)blockIdx.x * P;
-  {
-    const int w1 = nid ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, w2 = nid ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int u = ub0 + 16 * t + 4 * lk + r;
-#pragma unroll
-        for (int j = 0; j < 5; j++)
-          if (16 * j + li < NOBS) g[w1 + u * NOBS + 16 * j + li] = gw1[t][j][r];
-#pragma unroll
-        for (int j = 0; j < 4; j++) g[w2 + u * H + 16 * j + li] = gw2[t][j][r];
-      }
-  }
-#pragma unroll
-  for (int bb = 0; bb < PERV; bb++) {
-    const int i = tid + bb * GRAD_THREADS;
-    if (i < NVEC) g[vec_offset(i)] = accv[bb];
-  }
-  if ((wave & 1) == 0) {
-    la = wave_sum(la);
-    lb = wave_sum(lb);
-    lc = wave_sum(lc);
-    ln = wave_sum(ln);
-    if (lane == 0) {
-      float* lp = A.lpart + (size_t)blockIdx.x * ACKPPO_NLOSS;
-      if (wave == 0) {
-        lp[0] = la;
-        lp[2] = lb;
-        lp[3] = lc;
-        lp[4] = ln;
-        lp[5] = lp[6] = lp[7] = 0.0f;
-      } else {
-        lp[1] = la;
-      }
-    }
-  }
-  PSTAMP(15);
-}
-
-// ---- ackppo_grad, one net per workgroup (default, AK_PPO_GRAD1): workgroup 2 t + net takes the
-// actor (net 0) or the critic (net 1) of tile t. Its LDS (one net's weights, the tile and its
-// activations, ~78 KB) lets TWO workgroups share a CU, so one workgroup's barrier waits and memory
-// latencies hide under the other's MFMA / VALU work (the two-net workgroup of ackppo_grad_kernel
-// filled a CU's LDS alone: 4 waves per CU, one per SIMD). Wave w owns unit tile w (16 units) of its
+// ---- ackppo_grad: one net per workgroup. Workgroup 2 t + net takes the actor (net 0) or the critic
+// (net 1) of 32-sample tile t. Its LDS (one net's weights, the tile and its activations, ~78 KB) lets
+// TWO workgroups share a CU, so one workgroup's barrier waits and memory latencies hide under the
+// other's MFMA / VALU work (round 3's two-net workgroup filled a CU's LDS alone: 4 waves per CU, one
+// per SIMD; 26.6 -> 23.8 us per 8192-sample minibatch). Wave w owns unit tile w (16 units) of its
 // net in every product, for both 16-sample halves of the tile. D1 overwrites H1 in place once the
 // W2 gradient has read H1 (two barriers), which is what brings the footprint under 80 KB.
-#ifndef AK_PPO_GRAD1
-#define AK_PPO_GRAD1 1
-#endif
 namespace g1 {
 constexpr int T = 32, LDP = 36;  // samples per tile, padded tile row (floats)
 // weights: W1T [80][64] = [k][unit], XOR-swizzled as w1t_at (64-wide rows: the 16-bank groups of
@@ -735,36 +418,128 @@ constexpr int TOTAL = GA + 4 * LDP;
 static_assert(TOTAL * 4 * 2 <= 160 * 1024, "two one-net grad workgroups must share a CU's 160 KiB LDS");
 __device__ __forceinline__ int w1t(int k, int u) { return W1T + k * H + (u ^ (16 * (k & 3)) ^ ((k >> 2) & 15)); }
 __device__ __forceinline__ int w2(int u, int k) { return W2 + w2_at(u, k); }
-constexpr int MAX_TILES = GRAD_MAX_BLOCKS;  // partial rows: one per tile, as ackppo_grad_kernel
+constexpr int MAX_TILES = GRAD_MAX_BLOCKS;  // partial rows: one per tile (both nets' workgroups write it)
 }  // namespace g1
+#ifndef AK_PPO_GRAD2
+#define AK_PPO_GRAD2 0
+#endif
+namespace g2 {
+constexpr int T = 64;                         // samples per workgroup tile
+// weights, row-major with padded rows (no swizzle: every MFMA operand address is a per-lane base
+// plus an immediate): W1 [64][84] (inputs 79.. zero), W2 [64][68] and its transpose W2T [64][68]
+// (A operands of layer 2 and of W2^T D2); the stride's residue (20, 4 mod 64) spreads a read of 16
+// rows x 4 columns over 64 banks
+constexpr int S1 = 84, S2 = 68;
+constexpr int W1 = 0, W2 = W1 + H * S1, W2T = W2 + H * S2, B1 = W2T + H * S2, B2 = B1 + H;
+constexpr int HW = B2 + H;                    // heads: actor [2][64] (critic [1][64])
+constexpr int HB = HW + 2 * H;                // actor: b[2], log_std[2] (critic: b[1])
+constexpr int WEND = HB + 4;
+constexpr int XS = 80 * 16, HS = 64 * 16;     // per wave: X [80][16], H [64][16] (H1 -> D1), G [64][16] (H2 -> D2)
+constexpr int VS = 4 * 16;                    // per wave: gmu [2][16], glog [2][16] (critic: gv [16])
+constexpr int WSCR = XS + 2 * HS + VS;
+constexpr int SCR = WEND;                     // per-wave scratch after the weights
+constexpr int TOTAL = SCR + 4 * WSCR;
+// the end-of-kernel reduction reuses the whole LDS: [4 waves][64][80] (gW1 and the b1 column), then
+// [4 waves][64][VROW] (gW2, b2, head weights)
+constexpr int VROW = 64 + 1 + 2;
+static_assert(4 * 64 * 80 <= TOTAL && 4 * 64 * VROW + 16 <= TOTAL, "reduction scratch");
+static_assert(TOTAL * 4 <= 160 * 1024, "grad2 workgroup LDS");
+// [row][sample] tile swizzle: the sample index XORed with 4 ((row >> 2) & 3), so both MFMA read
+// patterns -- B[k][sample] (4 rows x 16 samples) and B[sample][row] (16 rows x 4 samples) -- hit 64
+// distinct banks
+__device__ __forceinline__ int sw(int row, int s) { return row * 16 + (s ^ (4 * ((row >> 2) & 3))); }
+}  // namespace g2
 
-__device__ __forceinline__ void stage_net(const float* __restrict__ p, float* w, int net) {
+// the staging of one net's weights; with an update (GradArgs::upd), each weight is first replaced by
+// its Adam step (adam_elem) -- the values the unfused ackppo_adam would have written -- and the
+// workgroup whose row is (element index mod rows) writes the new parameter and moments back
+template <bool UPD>
+__device__ __forceinline__ float stage_w4(const GradArgs& A, const AdamK& k, int off, int i4, int row, int nrow,
+                                          float4& out) {
+  const float4 pv = *reinterpret_cast<const float4*>(A.params + off + 4 * i4);
+  if constexpr (!UPD) {
+    out = pv;
+    return 0.0f;
+  } else {
+    const float4 gv = *reinterpret_cast<const float4*>(A.upd + off + 4 * i4);
+    const float4 mv = *reinterpret_cast<const float4*>(A.m_in + off + 4 * i4);
+    const float4 vv = *reinterpret_cast<const float4*>(A.v_in + off + 4 * i4);
+    float4 pn, mn, vn;
+    adam_elem(k, pv.x, gv.x, mv.x, vv.x, pn.x, mn.x, vn.x);
+    adam_elem(k, pv.y, gv.y, mv.y, vv.y, pn.y, mn.y, vn.y);
+    adam_elem(k, pv.z, gv.z, mv.z, vv.z, pn.z, mn.z, vn.z);
+    adam_elem(k, pv.w, gv.w, mv.w, vv.w, pn.w, mn.w, vn.w);
+    if (i4 % nrow == row) {
+      *reinterpret_cast<float4*>(A.p_out + off + 4 * i4) = pn;
+      *reinterpret_cast<float4*>(A.m_out + off + 4 * i4) = mn;
+      *reinterpret_cast<float4*>(A.v_out + off + 4 * i4) = vn;
+    }
+    out = pn;
+    return 0.0f;
+  }
+}
+template <bool UPD>
+__device__ __forceinline__ float stage_w1(const GradArgs& A, const AdamK& k, int idx, int row, int nrow) {
+  const float pv = A.params[idx];
+  if constexpr (!UPD) {
+    return pv;
+  } else {
+    float pn, mn, vn;
+    adam_elem(k, pv, A.upd[idx], A.m_in[idx], A.v_in[idx], pn, mn, vn);
+    if (idx == ACKPPO_OFF_LOG_STD || idx == ACKPPO_OFF_LOG_STD + 1) pn = ls_floor(k, pn);
+    if (idx % nrow == row) {
+      A.p_out[idx] = pn;
+      A.m_out[idx] = mn;
+      A.v_out[idx] = vn;
+    }
+    return pn;
+  }
+}
+// LDS weight layouts of the two grad kernels: ackppo_grad1 (g1: W1T swizzled, W2 swizzled) and
+// ackppo_grad2 (g2: padded row-major W1, W2 and W2^T)
+struct L1 {
+  static __device__ __forceinline__ void w1(float* w, int u, int k, float x) { w[g1::w1t(k, u)] = x; }
+  static __device__ __forceinline__ void w2(float* w, int u, int k, float x) { w[g1::w2(u, k)] = x; }
+  static constexpr int B1 = g1::B1, B2 = g1::B2, HW = g1::HW, HB = g1::HB;
+};
+struct L2 {
+  static __device__ __forceinline__ void w1(float* w, int u, int k, float x) { w[g2::W1 + u * g2::S1 + k] = x; }
+  static __device__ __forceinline__ void w2(float* w, int u, int k, float x) {
+    w[g2::W2 + u * g2::S2 + k] = x;
+    w[g2::W2T + k * g2::S2 + u] = x;
+  }
+  static constexpr int B1 = g2::B1, B2 = g2::B2, HW = g2::HW, HB = g2::HB;
+};
+template <bool UPD, class LY = L1>
+__device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, float* w, int net, int row, int nrow) {
   // all global loads first (one latency), then the LDS writes: W1 (float4 rows of 79 inputs)
   // transposed and swizzled, W2 swizzled, the short vectors
   constexpr int N1 = H * NOBS / 4, IT1 = (N1 + GRAD_THREADS - 1) / GRAD_THREADS, IT2 = H * H / 4 / GRAD_THREADS;
   const int tid = threadIdx.x;
-  const float* w1 = p + (net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1);
-  const float* w2 = p + (net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2);
+  const int o1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, o2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
   float4 v[IT1], v2[IT2];
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
     const int i = tid + j * GRAD_THREADS;
-    if (i < N1) v[j] = reinterpret_cast<const float4*>(w1)[i];
+    if (i < N1) stage_w4<UPD>(A, k, o1, i, row, nrow, v[j]);
   }
+  if constexpr (UPD) __builtin_amdgcn_sched_barrier(0);  // W1's four arrays, then W2's: bounded registers
 #pragma unroll
-  for (int j = 0; j < IT2; j++) v2[j] = reinterpret_cast<const float4*>(w2)[tid + j * GRAD_THREADS];
+  for (int j = 0; j < IT2; j++) stage_w4<UPD>(A, k, o2, tid + j * GRAD_THREADS, row, nrow, v2[j]);
   __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the scatter (one memory latency)
   // short vectors: threads 0-63 b1, b2 and the head rows; 64-67 the head biases / log_std
   float b1 = 0.f, b2 = 0.f, hw0 = 0.f, hw1 = 0.f, hs = 0.f;
   if (tid < H) {
-    b1 = p[(net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + tid];
-    b2 = p[(net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + tid];
-    hw0 = p[(net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W) + tid];
-    if (!net) hw1 = p[ACKPPO_OFF_ACT_W + H + tid];
+    b1 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + tid, row, nrow);
+    b2 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + tid, row, nrow);
+    hw0 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W) + tid, row, nrow);
+    if (!net) hw1 = stage_w1<UPD>(A, k, ACKPPO_OFF_ACT_W + H + tid, row, nrow);
   }
   const int sc = tid - H;  // actor: 0, 1 action_net.bias, 2, 3 log_std; critic: 0 value_net.bias
   const bool has_sc = sc >= 0 && sc < (net ? 1 : 4);
-  if (has_sc) hs = p[net ? ACKPPO_OFF_VAL_B : (sc < 2 ? ACKPPO_OFF_ACT_B + sc : ACKPPO_OFF_LOG_STD + sc - 2)];
+  if (has_sc)
+    hs = stage_w1<UPD>(A, k, net ? ACKPPO_OFF_VAL_B : (sc < 2 ? ACKPPO_OFF_ACT_B + sc : ACKPPO_OFF_LOG_STD + sc - 2),
+                       row, nrow);
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
     const int i = tid + j * GRAD_THREADS;
@@ -772,26 +547,26 @@ __device__ __forceinline__ void stage_net(const float* __restrict__ p, float* w,
       const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        const int r = 4 * i + c, u = r / NOBS, k = r - u * NOBS;
-        w[g1::w1t(k, u)] = e[c];
+        const int r = 4 * i + c, u = r / NOBS, kk = r - u * NOBS;
+        LY::w1(w, u, kk, e[c]);
       }
     }
   }
-  if (tid < H) w[g1::w1t(NOBS, tid)] = 0.0f;  // k row 79: the zero pad of the 80-deep layer-1 product
+  if (tid < H) LY::w1(w, tid, NOBS, 0.0f);  // input 79: the zero pad of the 80-deep layer-1 product
 #pragma unroll
   for (int j = 0; j < IT2; j++) {
-    const int i = 4 * (tid + j * GRAD_THREADS), u = i / H, k = i - u * H;
+    const int i = 4 * (tid + j * GRAD_THREADS), u = i / H, kk = i - u * H;
     const float e[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w};
 #pragma unroll
-    for (int c = 0; c < 4; c++) w[g1::w2(u, k + c)] = e[c];
+    for (int c = 0; c < 4; c++) LY::w2(w, u, kk + c, e[c]);
   }
   if (tid < H) {
-    w[g1::B1 + tid] = b1;
-    w[g1::B2 + tid] = b2;
-    w[g1::HW + tid] = hw0;
-    w[g1::HW + H + tid] = hw1;
+    w[LY::B1 + tid] = b1;
+    w[LY::B2 + tid] = b2;
+    w[LY::HW + tid] = hw0;
+    w[LY::HW + H + tid] = hw1;
   }
-  if (has_sc) w[g1::HB + sc] = hs;
+  if (has_sc) w[LY::HB + sc] = hs;
 }
 
 __device__ __forceinline__ float row_sum_t(const float* a) {  // 32 samples of one LDS tile row
@@ -841,8 +616,10 @@ __device__ __forceinline__ int vec_offset_g1(int net, int i) {
   return i < 192 ? ACKPPO_OFF_VAL_W + (i - 128) : ACKPPO_OFF_VAL_B;
 }
 
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kernel(GradArgs A) {
+template <bool UPD>
+__device__ __forceinline__ void grad1(const GradArgs& A) {
   using namespace g1;
+  PRSTAMP(13);
   PSTAMP(0);
   extern __shared__ float tl[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -886,7 +663,13 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kerne
   };
 
   if (tile0 < ntiles) loads(tile0);
-  stage_net(A.params, w, net);
+  AdamK ak{};
+  if constexpr (UPD) {  // the pending Adam step: the global norm first (every workgroup, same order)
+    const float norm = grad_norm256(A.upd, A.scale, tl + X);
+    ak = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
+    if (blockIdx.x == 0 && tid == 0 && A.norm_out) A.norm_out[0] = norm;
+  }
+  stage_net<UPD>(A, ak, w, net, tile0, tstride);
 
   f4v gw1[5], gw2[4];
 #pragma unroll
@@ -1123,7 +906,358 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kerne
     }
   }
   PSTAMP(15);
+  PRSTAMP(14);
 }
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kernel(GradArgs A) { grad1<false>(A); }
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1u_kernel(GradArgs A) { grad1<true>(A); }
+
+// ---- ackppo_grad, one net per workgroup, 16 samples per WAVE (default, AK_PPO_GRAD2). Workgroup
+// 2 t + net takes the actor (net 0) or the critic (net 1) of 64-sample tile t; wave w carries samples
+// 16 w .. 16 w + 15 of the tile through the whole forward / backward pass on its own -- every product
+// is [units x its 16 samples] (MFMA tiles of 16 units), its activations live in its own LDS scratch,
+// so no workgroup barrier separates the layers (ackppo_grad1's waves shared a 32-sample tile by unit
+// tiles: seven barriers per tile, one wave's stall held all four). The workgroup's four waves sum
+// their weight gradients once, at the end, through LDS (fixed order), and write one half-row (their
+// net) of the tile's partial gradient row: 128 rows per 8192-sample minibatch instead of 256.
+// Folded into the products: the layer-1 bias gradient is the gW1 column of the pad input row 79 (set
+// to 1; its weights are 0), the layer-2 bias gradient an extra gW2 column tile of ones, the head
+// weights' gradients an MFMA of the per-sample head gradients with H2.
+
+template <bool UPD>
+__device__ __forceinline__ void grad2(const GradArgs& A) {
+  using namespace g2;
+  PRSTAMP(13);
+  PSTAMP(0);
+  extern __shared__ float tl[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int net = blockIdx.x & 1, tile0 = blockIdx.x >> 1, tstride = gridDim.x >> 1;
+  float* w = tl;
+  float* xs = tl + SCR + wave * WSCR;   // this wave's X, H, G, V scratch
+  float* hs1 = xs + XS;
+  float* gs2 = hs1 + HS;
+  float* vs = gs2 + HS;
+  const float invB = 1.0f / (float)A.batch;
+  const int ntiles = (A.batch + T - 1) / T;
+  const int li = lane & 15, lk = lane >> 4;
+  // the wave's 16 samples: lane (li, lk) gathers inputs k = lk, lk + 4, ... of sample li
+  float xg[20];
+  float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto loads = [&](int tile) __attribute__((always_inline)) {
+    const int s0 = tile * T + 16 * wave, nvalid = min(16, A.batch - s0);
+    const int sidx = A.idx[min(s0 + li, A.batch - 1)];  // a valid index for padding lanes too
+    const float* row = A.obs_rows + (size_t)sidx * NOBS;
+    const bool v = li < nvalid;
+#pragma unroll
+    for (int i = 0; i < 20; i++) {
+      const int k = lk + 4 * i;
+      const float x = row[min(k, NOBS - 1)];
+      xg[i] = k < NOBS ? (v ? x : 0.0f) : 1.0f;  // input row 79: the ones of the layer-1 bias gradient
+    }
+    if (net == 0) {
+      const float2 a = *reinterpret_cast<const float2*>(A.actions + 2 * (size_t)sidx);
+      const float o = A.old_logp[sidx], ad = A.adv[sidx];
+      hin[0] = v ? a.x : 0.0f;
+      hin[1] = v ? a.y : 0.0f;
+      hin[2] = v ? o : 0.0f;
+      hin[3] = v ? ad : 0.0f;
+    } else {
+      const float rt = A.ret[sidx];
+      hin[0] = v ? rt : 0.0f;
+    }
+  };
+  if (tile0 < ntiles) loads(tile0);
+  AdamK ak{};
+  if constexpr (UPD) {  // the pending Adam step: the global norm first (every workgroup, same order)
+    const float norm = grad_norm256(A.upd, A.scale, tl + SCR);
+    ak = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
+    if (blockIdx.x == 0 && tid == 0 && A.norm_out) A.norm_out[0] = norm;
+  }
+  stage_net<UPD, L2>(A, ak, w, net, tile0, tstride);
+  __syncthreads();  // the weights are staged (the only barrier before the final reduction)
+  PSTAMP(1);
+
+  // accumulators over the workgroup's tiles: gW1 [4 unit tiles][5 input tiles] (column 79 = b1),
+  // gW2 [4][4] (+ [4] ones column: b2), head weights [4 unit tiles] (rows 0-1 actor mu, row 0 critic)
+  f4v gw1[4][5], gw2[4][5], ghw[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+#pragma unroll
+    for (int j = 0; j < 5; j++) gw1[t][j] = gw2[t][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    ghw[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
+  float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;   // loss sums (lanes lk == 0: sample li)
+  float sab0 = 0.f, sab1 = 0.f, slg0 = 0.f, slg1 = 0.f;  // head bias / log_std gradient sums (actor; critic sab0)
+
+  for (int tile = tile0; tile < ntiles; tile += tstride) {
+    const int s0 = tile * T + 16 * wave, nvalid = min(16, A.batch - s0);
+    if (tile != tile0) loads(tile);
+#pragma unroll
+    for (int i = 0; i < 20; i++) xs[sw(lk + 4 * i, li)] = xg[i];
+    wave_lds_sync();
+    PSTAMP(2);
+    {  // layer 1: H1 [64 x 16] = tanh(W1 X + b1), four unit tiles
+      f4v a[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k0 = 0; k0 < 80; k0 += 4) {
+        const int k = k0 + lk;
+        const float b = xs[sw(k, li)];
+#pragma unroll
+        for (int t = 0; t < 4; t++) a[t] = mfma4(w[W1 + (16 * t + li) * S1 + k], b, a[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = 16 * t + 4 * lk + r;
+          hs1[sw(u, li)] = ftanh(a[t][r] + w[B1 + u]);
+        }
+    }
+    wave_lds_sync();
+    PSTAMP(3);
+    {  // layer 2: H2 [64 x 16] = tanh(W2 H1 + b2)
+      f4v a[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;
+        const float b = hs1[sw(k, li)];
+#pragma unroll
+        for (int t = 0; t < 4; t++) a[t] = mfma4(w[W2 + (16 * t + li) * S2 + k], b, a[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = 16 * t + 4 * lk + r;
+          gs2[sw(u, li)] = ftanh(a[t][r] + w[B2 + u]);
+        }
+    }
+    wave_lds_sync();
+    PSTAMP(4);
+    // heads: lane (sample li, quarter lk) sums 16 of the 64 inputs (the quarter's rows rotated by lk:
+    // conflict-free), two butterflies over lk; every lane of sample li then holds its head outputs
+    const bool hvalid = li < nvalid;
+    float gm0 = 0.0f, gm1 = 0.0f;  // dL/dmu (actor) or dL/dV (critic, gm0) of sample li
+    if (net == 0) {
+      float m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int k = 16 * lk + ((j + lk) & 15);
+        const float h = gs2[sw(k, li)];
+        m0 = fmaf(w[HW + k], h, m0);
+        m1 = fmaf(w[HW + H + k], h, m1);
+      }
+      m0 += __shfl_xor(m0, 16, 64);
+      m1 += __shfl_xor(m1, 16, 64);
+      m0 += __shfl_xor(m0, 32, 64);
+      m1 += __shfl_xor(m1, 32, 64);
+      const float mu0 = m0 + w[HB], mu1 = m1 + w[HB + 1];
+      const float ls0 = w[HB + 2], ls1 = w[HB + 3];
+      const float logp = gauss_term(hin[0], mu0, ls0) + gauss_term(hin[1], mu1, ls1);
+      const float lr = logp - hin[2];
+      const float r = fexp(lr);
+      const float adv = (hin[3] - A.stats[0]) * A.stats[1];
+      const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
+      const float l1 = adv * r, l2 = adv * rc;
+      // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
+      // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
+      const float glogp = hvalid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
+      const float iv0 = fexp(-2.0f * ls0), iv1 = fexp(-2.0f * ls1);
+      const float dv0 = hin[0] - mu0, dv1 = hin[1] - mu1;
+      gm0 = glogp * dv0 * iv0;
+      gm1 = glogp * dv1 * iv1;
+      const float gl0 = glogp * (dv0 * dv0 * iv0 - 1.0f), gl1 = glogp * (dv1 * dv1 * iv1 - 1.0f);
+      if (lk == 0) {
+        vs[li] = gm0;
+        vs[16 + li] = gm1;
+        sab0 += gm0;
+        sab1 += gm1;
+        slg0 += gl0;
+        slg1 += gl1;
+        if (hvalid) {
+          la += -fminf(l1, l2);
+          lb += (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
+          lc += (r - 1.0f) - lr;
+          ln += 1.0f;
+        }
+      }
+    } else {
+      float v = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int k = 16 * lk + ((j + lk) & 15);
+        v = fmaf(w[HW + k], gs2[sw(k, li)], v);
+      }
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      v += w[HB];
+      const float R = hin[0];
+      gm0 = hvalid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
+      if (lk == 0) {
+        vs[li] = gm0;
+        sab0 += gm0;
+        if (hvalid) la += (R - v) * (R - v);
+      }
+    }
+    wave_lds_sync();
+    PSTAMP(5);
+    // head weights' gradient: [rows d x 64] += gmu [d x 16 samples] . H2^T (before D2 replaces H2)
+#pragma unroll
+    for (int q0 = 0; q0 < 16; q0 += 4) {
+      const int q = q0 + lk;
+      const float a = (li < (net ? 1 : 2)) ? vs[16 * li + q] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < 4; t++) ghw[t] = mfma4(a, gs2[sw(16 * t + li, q)], ghw[t]);
+    }
+    // D2 = dL/dH2 (1 - H2^2) in place: lane (sample li, quarter lk) takes units 16 lk + ...
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int u = 16 * lk + ((j + lk) & 15);
+      const float h = gs2[sw(u, li)];
+      const float dh = net ? gm0 * w[HW + u] : fmaf(gm0, w[HW + u], gm1 * w[HW + H + u]);
+      gs2[sw(u, li)] = dh * (1.0f - h * h);
+    }
+    wave_lds_sync();
+    PSTAMP(6);
+    {  // gW2 [64 x 64] += D2 H1^T and b2 (ones column tile); d1 = W2^T D2 (layer-1 units x 16)
+#pragma unroll
+      for (int q0 = 0; q0 < 16; q0 += 4) {
+        const int q = q0 + lk;  // sample
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const float a = gs2[sw(16 * t + li, q)];
+#pragma unroll
+          for (int j = 0; j < 4; j++) gw2[t][j] = mfma4(a, hs1[sw(16 * j + li, q)], gw2[t][j]);
+          gw2[t][4] = mfma4(a, 1.0f, gw2[t][4]);
+        }
+      }
+      f4v d[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k0 = 0; k0 < H; k0 += 4) {
+        const int k = k0 + lk;  // layer-2 unit
+        const float b = gs2[sw(k, li)];
+#pragma unroll
+        for (int t = 0; t < 4; t++) d[t] = mfma4(w[W2T + (16 * t + li) * S2 + k], b, d[t]);
+      }
+      wave_lds_sync();  // every read of H1 above is done: D1 replaces it
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int u = 16 * t + 4 * lk + r;
+          const float h = hs1[sw(u, li)];
+          hs1[sw(u, li)] = d[t][r] * (1.0f - h * h);
+        }
+    }
+    wave_lds_sync();
+    PSTAMP(7);
+    // gW1 [64 x 80] += D1 X^T (column 79: the ones row = b1)
+#pragma unroll
+    for (int q0 = 0; q0 < 16; q0 += 4) {
+      const int q = q0 + lk;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const float a = hs1[sw(16 * t + li, q)];
+#pragma unroll
+        for (int j = 0; j < 5; j++) gw1[t][j] = mfma4(a, xs[sw(16 * j + li, q)], gw1[t][j]);
+      }
+    }
+    wave_lds_sync();  // the next tile overwrites X
+    PSTAMP(8);
+  }
+  // ---- the workgroup's sums over its four waves (fixed order), written as its net's half-row
+  const int row = tile0;
+  float* g = A.gpart + (size_t)row * P;
+  const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ob1 = net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1;
+  const int ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2, ob2 = net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2;
+  const int ohw = net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W;
+  __syncthreads();  // every wave's scratch is free
+  {  // gW1 + b1: [wave][unit][80]
+    float* r1 = tl + wave * 64 * 80;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int j = 0; j < 5; j++) r1[(16 * t + 4 * lk + r) * 80 + 16 * j + li] = gw1[t][j][r];
+    __syncthreads();
+    // wave w sums units 16 w ..: 1280 values, 20 per lane
+    for (int i = lane; i < 16 * 80; i += 64) {
+      const int u = 16 * wave + i / 80, k = i % 80, o = u * 80 + k;
+      const float s = (tl[o] + tl[64 * 80 + o]) + (tl[2 * 64 * 80 + o] + tl[3 * 64 * 80 + o]);
+      if (k < NOBS) g[ow1 + u * NOBS + k] = s;
+      else g[ob1 + u] = s;
+    }
+    __syncthreads();
+  }
+  {  // gW2 + b2 + head weights: [wave][unit][VROW]
+    constexpr int VR = VROW;
+    float* r2 = tl + wave * 64 * VR;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int u = 16 * t + 4 * lk + r;
+#pragma unroll
+        for (int j = 0; j < 4; j++) r2[u * VR + 16 * j + li] = gw2[t][j][r];
+        if (li == 0) r2[u * VR + 64] = gw2[t][4][r];  // b2 (every column of the ones tile holds it)
+      }
+    // head weights: ghw[t] rows d = 4 lk + r (lk == 0: d = r), columns = units 16 t + li
+    if (lk == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        r2[(16 * t + li) * VR + 65] = ghw[t][0];
+        r2[(16 * t + li) * VR + 66] = ghw[t][1];
+      }
+    }
+    // scalar sums (head bias, log_std): over the wave's lanes, then into the last four words
+    sab0 = wave_sum(sab0);
+    sab1 = wave_sum(sab1);
+    slg0 = wave_sum(slg0);
+    slg1 = wave_sum(slg1);
+    la = wave_sum(la);
+    lb = wave_sum(lb);
+    lc = wave_sum(lc);
+    ln = wave_sum(ln);
+    float* sc = tl + 4 * 64 * VR;
+    if (lane == 0) {
+      sc[8 * wave + 0] = sab0;
+      sc[8 * wave + 1] = sab1;
+      sc[8 * wave + 2] = slg0;
+      sc[8 * wave + 3] = slg1;
+      sc[8 * wave + 4] = la;
+      sc[8 * wave + 5] = lb;
+      sc[8 * wave + 6] = lc;
+      sc[8 * wave + 7] = ln;
+    }
+    __syncthreads();
+    for (int i = lane; i < 16 * VR; i += 64) {
+      const int u = 16 * wave + i / VR, k = i % VR, o = u * VR + k;
+      if (net && k == 66) continue;  // the critic has one head row
+      const float s = (tl[o] + tl[64 * VR + o]) + (tl[2 * 64 * VR + o] + tl[3 * 64 * VR + o]);
+      if (k < 64) g[ow2 + u * H + k] = s;
+      else if (k == 64) g[ob2 + u] = s;
+      else g[ohw + (k - 65) * H + u] = s;
+    }
+    if (tid < 8) {
+      const float s = (sc[tid] + sc[8 + tid]) + (sc[16 + tid] + sc[24 + tid]);
+      float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
+      if (net == 0) {
+        if (tid < 2) g[ACKPPO_OFF_ACT_B + tid] = s;
+        else if (tid < 4) g[ACKPPO_OFF_LOG_STD + tid - 2] = s;
+        else lp[tid == 4 ? 0 : tid - 3] = s;  // policy loss, clipped count, approx-kl sum, samples
+        if (tid == 0) lp[5] = lp[6] = lp[7] = 0.0f;
+      } else {
+        if (tid == 0) g[ACKPPO_OFF_VAL_B] = s;
+        if (tid == 4) lp[1] = s;  // value loss sum
+      }
+    }
+  }
+  PSTAMP(15);
+  PRSTAMP(14);
+}
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2_kernel(GradArgs A) { grad2<false>(A); }
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2u_kernel(GradArgs A) { grad2<true>(A); }
 
 // ---- ackppo_act: MFMA policy tile. 16 envs per 256-lane workgroup (4096 envs = 256 workgroups,
 // one per CU): the weights are staged as in ackppo_grad (transposed / swizzled), X [80][16],
@@ -1401,43 +1535,34 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
   }
 }
 
-#ifndef ADAM_THREADS
-#define ADAM_THREADS 1024  // 19 blocks; each forms the norm with 18 loads per thread (256: 73); ~4.7 vs 4.8 us
-#endif
-extern "C" __global__ void __launch_bounds__(ADAM_THREADS) ackppo_adam_kernel(float* params, const float* grad,
-                                                                              float* m, float* v, float scale,
-                                                                              float max_norm, float b1, float b2,
-                                                                              float eps, float step_size,
-                                                                              float bc2_sqrt, float* norm_out) {
-  constexpr int NW = ADAM_THREADS / 64;
-  __shared__ float red[NW];
-  const int tid = threadIdx.x;
-  // every block forms the global norm itself (75 KB from L2) instead of a second launch: per-thread
-  // sums, a shuffle tree per wave, then the NW wave sums in a fixed order from LDS behind one
-  // barrier (a 1024-wide LDS tree took 10 barriers)
-  float ss = 0.0f;
-#pragma unroll 8
-  for (int i = tid; i < P; i += ADAM_THREADS) {
-    const float gi = grad[i] * scale;
-    ss = fmaf(gi, gi, ss);
+// clip_grad_norm_ + Adam over the whole vector: 256-thread workgroups, each forming the global norm
+// itself (grad_norm256: the order ackppo_grad1u_kernel's fused update uses, so the two give the same
+// bits) and updating 256 float4 of parameters in place
+extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* params, const float* grad, float* m,
+                                                                     float* v, float scale, float max_norm, float b1,
+                                                                     float b2, float eps, float step_size,
+                                                                     float bc2_sqrt, float* norm_out, float lsmin) {
+  __shared__ float red[4];
+  const float norm = grad_norm256(grad, scale, red);
+  const AdamK k = adam_k(norm, scale, max_norm, b1, b2, eps, step_size, bc2_sqrt, lsmin);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= P / 4) return;
+  const float4 pv = reinterpret_cast<const float4*>(params)[j], gv = reinterpret_cast<const float4*>(grad)[j];
+  const float4 mv = reinterpret_cast<const float4*>(m)[j], vv = reinterpret_cast<const float4*>(v)[j];
+  float4 pn, mn, vn;
+  adam_elem(k, pv.x, gv.x, mv.x, vv.x, pn.x, mn.x, vn.x);
+  adam_elem(k, pv.y, gv.y, mv.y, vv.y, pn.y, mn.y, vn.y);
+  adam_elem(k, pv.z, gv.z, mv.z, vv.z, pn.z, mn.z, vn.z);
+  adam_elem(k, pv.w, gv.w, mv.w, vv.w, pn.w, mn.w, vn.w);
+  static_assert(ACKPPO_OFF_LOG_STD == 0, "log_std in the first float4");
+  if (j == 0) {
+    pn.x = ls_floor(k, pn.x);
+    pn.y = ls_floor(k, pn.y);
   }
-  ss = wave_sum(ss);
-  if ((tid & 63) == 0) red[tid >> 6] = ss;
-  __syncthreads();
-  float tot = 0.0f;
-#pragma unroll
-  for (int w = 0; w < NW; w++) tot += red[w];
-  const float norm = sqrtf(tot);
-  const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
-  if (blockIdx.x == 0 && tid == 0 && norm_out) norm_out[0] = norm;
-  const int i = blockIdx.x * ADAM_THREADS + tid;
-  if (i >= P) return;
-  const float gi = grad[i] * scale * coef;
-  const float mi = m[i] + (1.0f - b1) * (gi - m[i]);  // exp_avg.lerp_(grad, 1 - beta1)
-  const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-  m[i] = mi;
-  v[i] = vi;
-  params[i] -= step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
+  reinterpret_cast<float4*>(params)[j] = pn;
+  reinterpret_cast<float4*>(m)[j] = mn;
+  reinterpret_cast<float4*>(v)[j] = vn;
 }
 
 // ------------------------------------------------------------------ C-ABI
@@ -1456,8 +1581,10 @@ int launched(const char* what) {
   }
   return ACKPPO_OK;
 }
-constexpr size_t GRAD_LDS = (size_t)G_TOTAL * sizeof(float);
-constexpr size_t GRAD1_LDS = (size_t)g1::TOTAL * sizeof(float);
+#ifndef AK_GRAD1_LDS_PAD  // diagnostic builds: extra LDS per workgroup (e.g. one workgroup per CU)
+#define AK_GRAD1_LDS_PAD 0
+#endif
+constexpr size_t GRAD_LDS = (size_t)(AK_PPO_GRAD2 ? g2::TOTAL : g1::TOTAL) * sizeof(float) + AK_GRAD1_LDS_PAD;
 // hipFuncSetAttribute is applied per device: flags indexed by the caller's current device
 constexpr int MAX_DEV = 64;
 bool g_grad_attr[MAX_DEV] = {};
@@ -1475,6 +1602,30 @@ bool policy_lds_ready() {
     return false;
   g_policy_attr[dev] = true;
   return true;
+}
+bool g_grad1u_attr[MAX_DEV] = {};
+// ackppo_grad's launch: two workgroups (actor, critic) per partial row; with A.upd, the variant that
+// applies the pending Adam step while staging (ackppo_train)
+int grad_launch(const GradArgs& A, void* stream) {
+  const int dev = current_device();
+  if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
+  const bool upd = A.upd != nullptr;
+  bool& ready = upd ? g_grad1u_attr[dev] : g_grad_attr[dev];
+  if (!ready) {
+    const void* kern = AK_PPO_GRAD2 ? (upd ? (const void*)ackppo_grad2u_kernel : (const void*)ackppo_grad2_kernel)
+                                    : (upd ? (const void*)ackppo_grad1u_kernel : (const void*)ackppo_grad1_kernel);
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS) != hipSuccess)
+      return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
+    ready = true;
+  }
+  const int nblk = ackppo_grad_blocks(A.batch);
+  if (AK_PPO_GRAD2)
+    hipLaunchKernelGGL(upd ? ackppo_grad2u_kernel : ackppo_grad2_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
+                       GRAD_LDS, (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(upd ? ackppo_grad1u_kernel : ackppo_grad1_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
+                       GRAD_LDS, (hipStream_t)stream, A);
+  return launched("ackppo_grad");
 }
 }  // namespace
 
@@ -1614,26 +1765,14 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
     return fail(ACKPPO_EINVAL, "ackppo_grad: bad arguments");
   const int dev = current_device();
   if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
-  const void* kern = AK_PPO_GRAD1 ? (const void*)ackppo_grad1_kernel : (const void*)ackppo_grad_kernel;
-  const size_t lds = AK_PPO_GRAD1 ? GRAD1_LDS : GRAD_LDS;
-  if (!g_grad_attr[dev]) {
-    const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
-    g_grad_attr[dev] = true;
-  }
   GradArgs A{params, obs_rows, actions, old_log_prob, advantages, returns, idx, batch, stats, clip_range, ent_coef,
              vf_coef, grad_partial, loss_partial};
-  const int nblk = ackppo_grad_blocks(batch);  // partial rows
-  if (AK_PPO_GRAD1)  // two workgroups (actor, critic) per partial row
-    hipLaunchKernelGGL(ackppo_grad1_kernel, dim3(2 * nblk), dim3(GRAD_THREADS), lds, (hipStream_t)stream, A);
-  else
-    hipLaunchKernelGGL(ackppo_grad_kernel, dim3(nblk), dim3(GRAD_THREADS), lds, (hipStream_t)stream, A);
-  return launched("ackppo_grad");
+  return grad_launch(A, stream);
 }
 
 int ackppo_grad_blocks(int batch) {
   if (batch <= 0) return 0;
-  const int tiles = (batch + GT - 1) / GT;
+  const int tiles = (batch + (AK_PPO_GRAD2 ? g2::T : g1::T) - 1) / (AK_PPO_GRAD2 ? g2::T : g1::T);
   return tiles < GRAD_MAX_BLOCKS ? tiles : GRAD_MAX_BLOCKS;
 }
 
@@ -1661,14 +1800,23 @@ int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, floa
   return reduce_launch(grad_partial, loss_partial, nblk, ent_coef, grad, loss, 0, stream);
 }
 
+namespace {
+int adam_launch(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
+                float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
+                float* grad_norm_out, float lsmin, void* stream) {
+  if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(ACKPPO_EINVAL, "ackppo_adam: bad arguments");
+  hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P / 4 + 255) / 256), dim3(256), 0, (hipStream_t)stream, params, grad,
+                     exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
+                     grad_norm_out, lsmin);
+  return launched("ackppo_adam");
+}
+}  // namespace
+
 int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
                 float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
                 float* grad_norm_out, void* stream) {
-  if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(ACKPPO_EINVAL, "ackppo_adam: bad arguments");
-  hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P + ADAM_THREADS - 1) / ADAM_THREADS), dim3(ADAM_THREADS), 0, (hipStream_t)stream, params, grad,
-                     exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
-                     grad_norm_out);
-  return launched("ackppo_adam");
+  return adam_launch(params, grad, exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size,
+                     bc2_sqrt, grad_norm_out, -INFINITY, stream);
 }
 
 int ackppo_epoch(float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
@@ -1709,11 +1857,12 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
   const bool dp = d->allreduce != nullptr;
   if ((d->world > 1 && !dp) || (dp && !d->moments))
     return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
+  const bool fuse = d->params2 && d->exp_avg2 && d->exp_avg_sq2;
   const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
     return fail(ACKPPO_EHIP, "ackppo_train: hipMemsetAsync(loss_acc)");
-  if (S == 0) return ACKPPO_OK;
+  if (S == 0 || d->n_epochs == 0) return ACKPPO_OK;
   const float scale = 1.0f / (float)d->world;
   int rc;
   auto coll = [&](void* buf, int64_t count, int dtype, const char* what) -> int {
@@ -1726,6 +1875,17 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
       return ACKPPO_EHIP;
     }
     return ACKPPO_OK;
+  };
+  // parameter / moment vectors: [0] the caller's, [1] the scratch (fused updates alternate)
+  float* pv[2] = {d->params, d->params2};
+  float* mv[2] = {d->exp_avg, d->exp_avg2};
+  float* vv[2] = {d->exp_avg_sq, d->exp_avg_sq2};
+  int cur = 0;
+  bool pending = false;  // an Adam step whose gradient is in d->grad, not yet applied
+  double t = 0.0;
+  auto adam_scalars = [&](double tt, float& step_size, float& bc2) {  // torch's bias corrections, float64
+    step_size = (float)(d->learning_rate / (1.0 - pow(d->beta1, tt)));
+    bc2 = (float)sqrt(1.0 - pow(d->beta2, tt));
   };
   for (int ep = 0; ep < d->n_epochs; ep++) {
     if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
@@ -1741,19 +1901,54 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     }
     for (int m = 0; m < nmb; m++) {
       const int nb = S - m * B < B ? S - m * B : B;
-      if ((rc = ackppo_grad(d->params, d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns,
-                            d->perm + (size_t)m * B, nb, d->stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef,
-                            d->grad_partial, d->loss_partial, stream)))
-        return rc;
+      GradArgs A{pv[cur], d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, d->perm + (size_t)m * B, nb,
+                 d->stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial};
+      if (pending) {  // fused: the previous minibatch's Adam step, applied while this launch stages
+        A.upd = d->grad;
+        A.m_in = mv[cur];
+        A.v_in = vv[cur];
+        A.p_out = pv[cur ^ 1];
+        A.m_out = mv[cur ^ 1];
+        A.v_out = vv[cur ^ 1];
+        A.scale = scale;
+        A.max_norm = d->max_grad_norm;
+        A.b1 = (float)d->beta1;
+        A.b2 = (float)d->beta2;
+        A.eps = d->eps;
+        adam_scalars(t, A.step_size, A.bc2_sqrt);
+        A.norm_out = d->grad_norm_out;
+        A.lsmin = d->log_std_min;
+        cur ^= 1;
+      }
+      if ((rc = grad_launch(A, stream))) return rc;
       if ((rc = reduce_launch(d->grad_partial, d->loss_partial, ackppo_grad_blocks(nb), d->ent_coef, d->grad,
                               d->loss_acc, 1, stream)))
         return rc;
       if (dp && (rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
-      const double t = (double)(d->adam_step0 + (int64_t)ep * nmb + m + 1);  // torch's bias corrections (float64)
-      if ((rc = ackppo_adam(d->params, d->grad, d->exp_avg, d->exp_avg_sq, scale, d->max_grad_norm, (float)d->beta1,
-                            (float)d->beta2, d->eps, (float)(d->learning_rate / (1.0 - pow(d->beta1, t))),
-                            (float)sqrt(1.0 - pow(d->beta2, t)), d->grad_norm_out, stream)))
-        return rc;
+      t = (double)(d->adam_step0 + (int64_t)ep * nmb + m + 1);
+      if (fuse) {
+        pending = true;
+      } else {
+        float ss, bc2;
+        adam_scalars(t, ss, bc2);
+        if ((rc = adam_launch(pv[cur], d->grad, mv[cur], vv[cur], scale, d->max_grad_norm, (float)d->beta1,
+                              (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream)))
+          return rc;
+      }
+    }
+  }
+  if (pending) {  // the last step, in place, then the result back into the caller's vectors
+    float ss, bc2;
+    adam_scalars(t, ss, bc2);
+    if ((rc = adam_launch(pv[cur], d->grad, mv[cur], vv[cur], scale, d->max_grad_norm, (float)d->beta1,
+                          (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream)))
+      return rc;
+    if (cur == 1) {
+      const size_t bytes = ACKPPO_NPARAM * sizeof(float);
+      if (hipMemcpyAsync(d->params, pv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(d->exp_avg, mv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(d->exp_avg_sq, vv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(ACKPPO_EHIP, "ackppo_train: copying the result back");
     }
   }
   return ACKPPO_OK;

@@ -109,7 +109,7 @@ class PPO:
                  clip_range_vf=None, normalize_advantage: bool = True, ent_coef: float = 0.0, vf_coef: float = 0.5,
                  max_grad_norm: float = 0.5, target_kl=None, seed: int | None = None, verbose: int = 0,
                  policy_kwargs: dict | None = None, device=None, world: int | None = None, rank: int | None = None,
-                 fused_rollout: bool | None = None, collective: str | None = None):
+                 fused_rollout: bool | None = None, collective: str | None = None, log_std_min: float | None = None):
         if policy != "MlpPolicy":
             raise ValueError("only 'MlpPolicy' (the reference's policy, train.py:126) is provided")
         if clip_range_vf is not None or target_kl is not None:
@@ -120,6 +120,9 @@ class PPO:
             raise NotImplementedError("schedules: the reference uses constant learning_rate / clip_range")
         self.env = env
         self.sim = env.sim
+        # opt-in entropy floor (NOT an SB3 argument; None = SB3): log_std held >= log_std_min after every
+        # Adam step, so the policy's spread cannot collapse (include/ackppo.h ackppo_train_desc)
+        self.log_std_min = log_std_min
         # the policy-in-the-loop rollout in one launch (ackphys_ppo_rollout) where the kernels provide
         # it -- contacts on, the quad mapping, pre-integration observations -- else one act launch and
         # one step launch per step; both give the same rollout bit for bit
@@ -162,6 +165,8 @@ class PPO:
         self.gpart = torch.zeros(nblk, NPARAM, **f32)  # pad words are never written: zero once
         self.lpart = torch.zeros(nblk, NLOSS, **f32)
         self.grad = torch.zeros(NPARAM, **f32)
+        # the alternate parameter / moment vectors of the fused Adam step (ackppo_train_desc params2 ...)
+        self.scratch = torch.zeros(3, NPARAM, **f32)
         self.loss = torch.zeros(NLOSS, **f32)
         self.loss_acc = torch.zeros(NLOSS, **f32)
         self.gnorm = torch.zeros(1, **f32)
@@ -291,7 +296,16 @@ class PPO:
         d.grad_partial, d.loss_partial = self.gpart.data_ptr(), self.lpart.data_ptr()
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
         d.world = self.world
+        d.log_std_min = float("-inf") if self.log_std_min is None else float(self.log_std_min)
+        self.set_fuse_adam(True, d)
         return d
+
+    def set_fuse_adam(self, on: bool, d=None):
+        """Each minibatch's Adam step applied by the next gradient launch (one launch less per
+        minibatch, the same bits) -- on by default; off: a separate ackppo_adam launch each."""
+        d = self._desc if d is None else d
+        ptrs = [t.data_ptr() for t in self.scratch] if on else [None, None, None]
+        d.params2, d.exp_avg2, d.exp_avg_sq2 = ptrs
 
     def set_collective(self, kind: str | None):
         """The update's all-reduce hook (shard.TrainerCollective): "rccl", "host", None = the

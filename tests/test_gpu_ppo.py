@@ -324,14 +324,15 @@ def test_train_paths_bit_identical():
     """PPO.train is one ackppo_train call. Its single-rank sequence (no hook), the data-parallel
     sequence over a one-rank native RCCL communicator (ackppo_rccl_allreduce: the world > 1 path with
     real RCCL calls) and over the host-staged hook (the gloo rehearsals' path, a no-op at world 1)
-    give bit-identical parameters, Adam moments and loss statistics -- and so does the C-level
-    ackppo_epoch loop of the same epochs."""
+    give bit-identical parameters, Adam moments and loss statistics -- with each Adam step fused into
+    the next gradient launch (default) or launched on its own."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     out = []
-    for coll in (None, "rccl", "host"):
+    for coll, fuse in ((None, True), ("rccl", True), ("host", True), (None, False), ("rccl", False)):
         venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
         model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01, collective=coll)
+        model.set_fuse_adam(fuse)
         assert (model.collective is None) == (coll is None)
         model.learn(total_timesteps=2 * 16 * 256)
         out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
@@ -343,7 +344,8 @@ def test_train_paths_bit_identical():
 
 
 def test_train_matches_epoch_calls():
-    """ackppo_train (world 1, no hook) = per epoch ackppo_permutation + ackppo_adv_stats + ackppo_epoch."""
+    """ackppo_train (world 1, no hook, the Adam steps fused into the gradient launches) = per epoch
+    ackppo_permutation + ackppo_adv_stats + ackppo_epoch (grad -> reduce -> adam launches), bit for bit."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
@@ -454,3 +456,22 @@ def test_ppo_learns_the_variant_task():
     s1, steps, _ = evaluate(model, horizon=1000, **kw)
     print("success", s0, "->", s1, "steps to goal", steps)
     assert s0 == 0.0 and s1 >= 0.05
+
+
+def test_log_std_floor():
+    """The opt-in entropy floor (log_std_min; include/ackppo.h): after every Adam step log_std >= the
+    floor -- a policy started below it is lifted to it at the first update -- the same bits with the
+    Adam step fused into the gradient launch or on its own; None leaves the SB3 update untouched."""
+    from mujoco_playground_amd.rl import make_ackermann_env
+    from mujoco_playground_amd.rl.ppo import PPO
+    out = []
+    for fuse in (True, False):
+        venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=2, seed=3, log_std_min=-0.5)
+        model.set_fuse_adam(fuse)
+        model.params[:2] = -2.0
+        model.learn(total_timesteps=2 * 16 * 256)
+        ls = model.params[:2].cpu().numpy()
+        assert (ls >= -0.5).all(), ls
+        out.append(model.params.cpu().numpy())
+    np.testing.assert_array_equal(out[0], out[1])

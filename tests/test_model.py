@@ -113,3 +113,28 @@ def test_rollout_rejects_bad_arguments_without_touching_the_gpu():
     assert rc == -1 and b"k_steps" in L.ackphys_last_error()
     rc = L.ackphys_rollout(dummy, 3, None, dummy, dummy, dummy, dummy, dummy, None, None, None, 0, 0, 0, None)
     assert rc == -1 and b"NULL" in L.ackphys_last_error()
+
+
+def test_ctypes_structs_match_the_c_layouts(tmp_path):
+    """The ctypes mirrors of the C-ABI structs (_lib.TrainDesc = ackppo_train_desc, _lib.EnvParams =
+    ackphys_env_params) have the C compiler's size and field offsets: a mismatch hands the library
+    garbage (a misplaced field once read a scratch pointer as the all-reduce hook)."""
+    import subprocess
+    checks = {"ackppo_train_desc": ("ackppo.h", _lib.TrainDesc), "ackphys_env_params": ("ackphys.h", _lib.EnvParams)}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "include/ackppo.h"', '#include "include/ackphys.h"',
+           "int main(void) {"]
+    for cname, (_, py) in checks.items():
+        src.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _t in py._fields_:
+            src.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src.append("  return 0;\n}")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", _lib.REPO, str(c), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                               check=True).stdout.splitlines())
+    for cname, (_, py) in checks.items():
+        assert int(got[f"{cname} size"]) == C.sizeof(py), cname
+        for f, _t in py._fields_:
+            assert int(got[f"{cname} {f}"]) == getattr(py, f).offset, (cname, f)

@@ -67,34 +67,46 @@ if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "--stamps"):
         run(p)
 
 
-def stamps(path):
-    """Per-phase cycles of ackppo_grad from the PP_STAMPS build (median over workgroups)."""
+def stamps(path, batches=(8192, 4096)):
+    """Per-phase cycles of ackppo_grad from the PP_STAMPS build (median over workgroups), and the
+    launch's timeline from the 100 MHz clock (stamps 13 / 14: workgroup start / end): span, start
+    skew, median workgroup duration; for each minibatch size."""
     L = C.CDLL(path)
     p32, i32, f32 = C.c_void_p, C.c_int, C.c_float
     L.ackppo_grad.argtypes = [p32] * 7 + [i32, p32, f32, f32, f32, p32, p32, p32]
     L.ackppo_diag_set_stamps.argtypes = [p32]
-    S, B = 131072, 8192
+    S = 131072
     params = (torch.randn(NP) * 0.1).to(dev)
     obs, act = torch.randn(S, 79, device=dev), torch.randn(S, 2, device=dev)
     lp, adv, ret = torch.randn(S, device=dev), torch.randn(S, device=dev), torch.randn(S, device=dev)
     idx = torch.randperm(S, device=dev).to(torch.int32)
     stats = torch.tensor([0.0, 1.0], device=dev)
     L.ackppo_grad_blocks.argtypes = [C.c_int]
-    nblk = L.ackppo_grad_blocks(B)
-    gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
-    st = torch.zeros(16 * 2 * nblk, dtype=torch.int64, device=dev)  # grad1: two workgroups per row
-    L.ackppo_diag_set_stamps(P(st))
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for _ in range(3):
-        L.ackppo_grad(P(params), P(obs), P(act), P(lp), P(adv), P(ret), P(idx), B, P(stats), 0.2, 0.0, 0.5, P(gp),
-                      P(lpart), s)
-    torch.cuda.synchronize()
-    a = st.cpu().numpy().reshape(16, -1)
-    a = a[:, : int((a[0] != 0).sum())]
-    used = [k for k in range(16) if a[k].any()]
-    print("grad phases (median cycles per workgroup):",
-          {f"{used[i]}->{used[i + 1]}": int(np.median(a[used[i + 1]] - a[used[i]])) for i in range(len(used) - 1)},
-          "total", int(np.median(a[used[-1]] - a[used[0]])))
+    for B in batches:
+        nblk = L.ackppo_grad_blocks(B)
+        gp, lpart = torch.zeros(nblk, NP, device=dev), torch.zeros(nblk, 8, device=dev)
+        st = torch.zeros(16 * 2 * nblk, dtype=torch.int64, device=dev)  # grad1: two workgroups per row
+        L.ackppo_diag_set_stamps(P(st))
+        call = lambda: L.ackppo_grad(P(params), P(obs), P(act), P(lp), P(adv), P(ret), P(idx), B, P(stats), 0.2,  # noqa: E731
+                                     0.0, 0.5, P(gp), P(lpart), s)
+        for _ in range(3):
+            call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        a = st.cpu().numpy().reshape(16, -1)
+        a = a[:, : int((a[0] != 0).sum())]
+        used = [k for k in range(13) if a[k].any()]
+        ph = {f"{used[i]}->{used[i + 1]}": int(np.median(a[used[i + 1]] - a[used[i]])) for i in range(len(used) - 1)}
+        t0, t1 = a[13], a[14]
+        print(f"batch {B}: {a.shape[1]} workgroups, event-timed {e0.elapsed_time(e1) / 10 * 1e3:.1f} us; "
+              f"phases (median cycles per workgroup) {ph} total {int(np.median(a[used[-1]] - a[used[0]]))}; "
+              f"timeline (100 MHz): span {(t1.max() - t0.min()) / 100:.2f} us, start skew {(t0.max() - t0.min()) / 100:.2f} us, "
+              f"median workgroup {np.median(t1 - t0) / 100:.2f} us, max {(t1 - t0).max() / 100:.2f} us", flush=True)
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--stamps":

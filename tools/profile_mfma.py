@@ -19,7 +19,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "mujoco_playground_amd", "csrc", "build", "libackppo.so")
-KERNELS = ("ackppo_grad_kernel", "ackppo_act_kernel")
+KERNELS = ("ackppo_grad2_kernel", "ackppo_act_kernel")
 SIMDS, XCDS, F32_MFMA_PEAK_TFLOPS = 1024, 8, 157.3
 
 

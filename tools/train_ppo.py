@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--log-std-min", type=float, default=None,
+                    help="opt-in entropy floor: log_std held >= this after every Adam step (default: SB3, none)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     env_kw = dict(collision_threshold=a.collision_threshold, action_repeat=a.action_repeat,
@@ -92,7 +94,7 @@ def main():
     venv = make_ackermann_env(env_type="vec", num_envs=a.envs, device=dev, seed=a.seed,
                               max_episode_steps=a.max_episode_steps, **env_kw)
     model = PPO("MlpPolicy", venv, n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs, learning_rate=a.lr,
-                ent_coef=a.ent_coef, gamma=a.gamma, seed=a.seed)
+                ent_coef=a.ent_coef, gamma=a.gamma, seed=a.seed, log_std_min=a.log_std_min)
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     out = open(a.out, "w")
     hdr = {"config": vars(a), "fused_rollout": model.fused_rollout}
