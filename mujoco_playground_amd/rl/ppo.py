@@ -297,12 +297,15 @@ class PPO:
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
         d.world = self.world
         d.log_std_min = float("-inf") if self.log_std_min is None else float(self.log_std_min)
-        self.set_fuse_adam(True, d)
+        self.set_fuse_adam(False, d)
         return d
 
     def set_fuse_adam(self, on: bool, d=None):
-        """Each minibatch's Adam step applied by the next gradient launch (one launch less per
-        minibatch, the same bits) -- on by default; off: a separate ackppo_adam launch each."""
+        """on: each minibatch's Adam step applied by the next gradient launch while it stages the
+        weights (one launch less per minibatch, the same bits); off (default): a separate ackppo_adam
+        launch each. Measured (profiles/r04f_ppo_timing.log): 41.9 us per minibatch fused against
+        38.7 us -- every one of the 512 gradient workgroups re-derives its net's Adam step (four
+        parameter-sized reads and the global norm), which costs more than the launch it saves."""
         d = self._desc if d is None else d
         ptrs = [t.data_ptr() for t in self.scratch] if on else [None, None, None]
         d.params2, d.exp_avg2, d.exp_avg_sq2 = ptrs

@@ -15,7 +15,14 @@ for k in ("ackphys_step_nc_kernel", "ackphys_step_quad_kernel", "ackphys_step_ob
     i = s.find("\n" + k + ":"); j = s.index(".Lfunc_end", i)
     ops = [l.split()[0] for l in s[i:j].split("\n") if l.startswith("\t") and l.strip() and not l.strip().startswith((".", ";"))]
     c = collections.Counter(ops)
-    g = lambda f: re.search(r"\.set " + k + r"\." + f + r", (\d+)", s).group(1)
+    def g(f):  # kernels that call functions report max(own, callee's)
+        v = re.search(r"\.set " + k + r"\." + f + r", (.+)", s).group(1).strip()
+        if v.isdigit():
+            return v
+        nums = [int(x) for x in re.findall(r"\b(\d+)\b", v)]
+        callees = re.findall(r"(\.L\w+)\." + f, v)
+        nums += [int(re.search(re.escape(c) + r"\." + f + r", (\d+)", s).group(1)) for c in callees]
+        return str(max(nums)) if nums else v
     print(f"{k}: {len(ops)} instr, vgpr {g('num_vgpr')} agpr {g('num_agpr')} sgpr {g('numbered_sgpr')}, "
           f"v_mov {c['v_mov_b32_e32']}, agpr moves {c['v_accvgpr_write_b32'] + c['v_accvgpr_read_b32']}, "
           f"sgpr lane spills {c['v_readlane_b32'] + c['v_writelane_b32']}, scratch {sum(v for o, v in c.items() if o.startswith('scratch'))}, "

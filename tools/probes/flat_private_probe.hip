@@ -38,10 +38,12 @@ __device__ __forceinline__ float pick(const Chain& C, int t, const float* x) {
 }
 // slots visited as the kernels' FOR_QSLOTS does (a wave-uniform bit mask, loop not unrolled); the
 // result of slot t is written to its row of `rows` (LDS), read back for the return value
+__device__ __noinline__ void keep(Chain* c) { asm volatile("" ::"v"(c) : "memory"); }
 template <bool VAL>
 __device__ __forceinline__ float body(int t, int q, float* x, uint32_t wact) {
   Chain C;
   fill(C, q);
+  keep(&C);  // C's address escapes: it stays in private memory (as QChain did in the noinline build)
   float s = 0.0f;
 #pragma unroll 1
   for (uint32_t m = wact; m; m &= m - 1) {

@@ -19,7 +19,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "mujoco_playground_amd", "csrc", "build", "libackppo.so")
-KERNELS = ("ackppo_grad2_kernel", "ackppo_act_kernel")
+KERNELS = ("ackppo_grad1_kernel", "ackppo_act_kernel")
 SIMDS, XCDS, F32_MFMA_PEAK_TFLOPS = 1024, 8, 157.3
 
 
@@ -83,7 +83,7 @@ def main():
                   "mfma_util": busy / (gui / XCDS * SIMDS) if gui else None,
                   "mfma_util_rocprof_derived_pct": (sum(d.get("MfmaUtil", 0.0) for d in dv) / len(dv)) if dv else None,
                   "mfma_tflops": mops * 512 / (ns * 1e-9) / 1e12, "f32_mfma_peak_tflops": F32_MFMA_PEAK_TFLOPS,
-                  "workload": "tools/ppo_kbench.py: grad = one 8192-sample minibatch (256 workgroups), act = 4096 envs"}
+                  "workload": "tools/ppo_kbench.py: grad = one 8192-sample minibatch (512 one-net workgroups of 32 samples), act = 4096 envs"}
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "mfma_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
