@@ -326,6 +326,20 @@ CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md constants table
 STAMP_OVERHEAD = 0.11  # cycles the diagnostic build's LDS stamps add to the dynamics wave
 
 
+def valu_block(pmc, kern_ms: float):
+    """VALU issue share of a kernel from its committed PMC entry (None without one)."""
+    if not (pmc and pmc.get("valu_insts_per_wave_step")):
+        return None
+    # one wave alone issues a dependent VALU op every ~4 cycles (MI355X_MICROARCH.md constants
+    # table; tools/probes/launch_floor.py measures 4.1 cycles per op of a dependent FMA chain)
+    return {"insts_per_wave_step": pmc["valu_insts_per_wave_step"], "waves": pmc["SQ_WAVES"],
+            "issue_frac_of_kernel_time": pmc["valu_insts_per_wave_step"] * 4 / (kern_ms * 1e-3 * CLOCK_GHZ * 1e9),
+            "source": pmc["source"],
+            "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave "
+                    "dependent-op rate (4 cyc/op), per-wave average over the kernel's waves (contacts off: "
+                    "dynamics, observation and prep waves); the rest is dependency/memory latency"}
+
+
 def critical_path(kern_name: str, kern_ms: float):
     """The dynamics wave's dependent chain against the kernel time: cycles per step from the
     stamped diagnostic build (tools/stamps.py -> profiles/critical_path_latest.json), not this run."""
@@ -438,6 +452,9 @@ def main():
                     help="skip the rollout-buffer leg (the headline launch with per-step output slices)")
     ap.add_argument("--buffers", action="store_true",
                     help="time the headline launch with per-step output slices (tools/profile_pmc.py --buffers)")
+    ap.add_argument("--scene", default="flat", choices=["flat", "obstacles"],
+                    help="scene of the headline launch (profiling: tools/profile_pmc.py --obstacles); the "
+                         "driver's bench line is the flat scene")
     ap.add_argument("--check-launch", action="store_true",
                     help="ranks check the world and backend, print one JSON line and exit (no GPU work)")
     a = ap.parse_args()
@@ -474,7 +491,7 @@ def main():
     clock_warm(device, a.envs)
     sim, elapsed, kern_ms, rets, _ = run_gpu(a.envs, a.steps, a.warmup, contacts, rank, world, device,
                                              variant=a.variant, graph=a.graph, per_step=a.per_step,
-                                             buffers=a.buffers)
+                                             buffers=a.buffers, scene=a.scene)
     value = total_envs * a.steps / elapsed
 
     def per_step_leg(c, scene="flat"):
@@ -502,12 +519,29 @@ def main():
     bpe = algorithmic_bytes_per_env_step()
     kern = "quad" if (a.variant == "quad" or (a.variant == "auto" and contacts)) else ("" if contacts else "nc")
     kern = ("ackphys_rollout" if fused else "ackphys_step") + (f"_{kern}" if kern else "") + "_kernel"
+    if a.scene == "obstacles":
+        kern = "ackphys_rollout_obst8_kernel" if fused else "ackphys_step_obst_kernel"
     rollout_buffer = buffer_leg(contacts) if (fused and not a.no_buffer_leg) else None
+
+    def leg_roofline(kname, c, km):
+        """the roofline block of a non-headline leg: the same algorithmic-bytes HBM figure, the
+        counter bytes, VALU issue share and the dynamics wave's critical path where profiled"""
+        ach = bpe * a.envs / (km * 1e-3) / 1e9
+        pm = load_pmc(kname, c, a.steps)
+        return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "limiter": "valu-latency", "kernel": kname, "kernel_ms": km,
+                "traffic": (pm["hbm_bytes_per_step"] * a.steps if (pm and fused) else None),
+                "traffic_unit": "HBM bytes per launch (PMC, profiled separately)",
+                "counter_source": pm["source"] if pm else None,
+                "critical_path": critical_path(kname, km), "valu": valu_block(pm, km)}
     secondary = None
     if sec_run is not None:
         _, el2, km2, _, _ = sec_run
+        k2 = "quad" if (a.variant == "quad" or (a.variant == "auto" and not contacts)) else ("" if not contacts else "nc")
+        kern2 = "ackphys_rollout" + (f"_{k2}" if k2 else "") + "_kernel"
         secondary = {"contacts": not contacts, "value": total_envs * a.steps / el2, "ms_per_step": el2 * 1e3 / a.steps,
                      "kernel_ms": km2, "per_step_launch": per_step_leg(not contacts) if do_per_step else None,
+                     "roofline": leg_roofline(kern2, not contacts, km2) if fused else None,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS) if not contacts else a.warmup,
                      "flops": oracle_flops("configs[1] contacts off" if contacts else "configs[2] contacts on",
                                            total_envs * a.steps / el2)}
@@ -523,22 +557,14 @@ def main():
                      "per_step_launch": per_step_leg(True, "obstacles") if do_per_step else None, "episodes": rets3,
                      "untimed_steps": max(a.warmup, SETTLE_STEPS),
                      "flops": oracle_flops("configs[4] obstacle scene, contacts on", total_envs * a.steps / el3),
+                     "roofline": leg_roofline("ackphys_rollout_obst8_kernel", True, km3) if fused else None,
                      "ppo": None if a.no_ppo else run_ppo(a.envs, rank, world, device, scene="obstacles")}
     parity = base = None
     if rank == 0 and not a.no_cpu:
         parity, base = cpu_leg(device, contacts, do_timing=(world == 1))
     achieved = bpe * a.envs / (kern_ms * 1e-3) / 1e9
     pmc = load_pmc(kern, contacts, a.steps)
-    valu = None
-    if pmc and pmc.get("valu_insts_per_wave_step"):
-        # one wave alone issues a dependent VALU op every ~4 cycles (MI355X_MICROARCH.md constants
-        # table; tools/probes/launch_floor.py measures 4.1 cycles per op of a dependent FMA chain)
-        valu = {"insts_per_wave_step": pmc["valu_insts_per_wave_step"], "waves": pmc["SQ_WAVES"],
-                "issue_frac_of_kernel_time": pmc["valu_insts_per_wave_step"] * 4 / (kern_ms * 1e-3 * CLOCK_GHZ * 1e9),
-                "source": pmc["source"],
-                "note": "fraction of the kernel's duration one wave spends issuing VALU at the lone-wave "
-                        "dependent-op rate (4 cyc/op), per-wave average over the kernel's waves (contacts off: "
-                        "dynamics, observation and prep waves); the rest is dependency/memory latency"}
+    valu = valu_block(pmc, kern_ms)
     hbm = {"nominal_bytes_per_step": bpe * a.envs,
            "counter_bytes_per_step": pmc.get("hbm_bytes_per_step") if pmc else None,
            "counter_source": pmc["source"] if pmc else None,

@@ -52,6 +52,7 @@ extern "C" {
 #define ACKPPO_OFF_VAL_B 18760    /* value_net.bias                    [1]     */
 #define ACKPPO_NPARAM 18764
 #define ACKPPO_NLOSS 8            /* loss partial words per workgroup (see ackppo_grad) */
+#define ACKPPO_WIMAGE 9728        /* floats per net of ackppo_train_desc::weight_image */
 
 #define ACKPPO_OK 0
 #define ACKPPO_EINVAL -1
@@ -215,6 +216,11 @@ typedef struct {
    * above this value after every Adam step, so the DiagGaussian's spread cannot collapse below
    * exp(log_std_min) */
   float log_std_min;
+  /* optional scratch, 2 * ACKPPO_WIMAGE floats (NULL: off): each net's gradient-kernel weight block
+   * in the kernel's LDS layout, written by every Adam step beside the parameters (and built from
+   * them when the call starts), so the gradient launches copy it into LDS with plain DMA instead of
+   * transposing the parameters. Same results bit for bit; ignored with the fused update (params2) */
+  float* weight_image;
 } ackppo_train_desc;
 
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch

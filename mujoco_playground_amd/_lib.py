@@ -64,6 +64,8 @@ class EnvParams(C.Structure):
                 ("action_repeat", C.c_int32), ("nohit_clear", C.c_int32), ("goal_cells", C.c_int32)]
 
 
+ACKPPO_WIMAGE = 9728  # floats per net of ackppo_train_desc::weight_image (include/ackppo.h)
+
 # ackppo_allreduce_fn (include/ackppo.h): SUM all-reduce in place of (buf, count, dtype, user, stream)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p)
 
@@ -81,7 +83,8 @@ class TrainDesc(C.Structure):
                 ("loss_partial", C.c_void_p), ("grad", C.c_void_p), ("loss_acc", C.c_void_p),
                 ("grad_norm_out", C.c_void_p), ("world", C.c_int), ("allreduce", C.c_void_p),
                 ("allreduce_user", C.c_void_p), ("params2", C.c_void_p), ("exp_avg2", C.c_void_p),
-                ("exp_avg_sq2", C.c_void_p), ("log_std_min", C.c_float)]
+                ("exp_avg_sq2", C.c_void_p), ("log_std_min", C.c_float),
+                ("weight_image", C.c_void_p)]
 
 
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:

@@ -45,17 +45,20 @@ __shared__ unsigned long long ak_stamp_lds[4][AK_NSTAMP];
     if ((threadIdx.x & 63) == 0) ak_stamp_lds[threadIdx.x >> 6][k] = _t;                  \
   } while (0)
 struct StampScope {
-  __device__ StampScope() {
+  bool on;
+  __device__ explicit StampScope(bool on_ = true) : on(on_) {
     if ((threadIdx.x & 63) == 0)
       for (int k = 0; k < AK_NSTAMP; k++) ak_stamp_lds[threadIdx.x >> 6][k] = 0;
   }
   __device__ ~StampScope() {
-    if ((threadIdx.x & 63) == 0)
+    if (on && (threadIdx.x & 63) == 0)
       for (int k = 0; k < AK_NSTAMP; k++)
         if (const unsigned long long v = ak_stamp_lds[threadIdx.x >> 6][k]) g_stamps[(size_t)k * gridDim.x + blockIdx.x] = v;
   }
 };
 #define STAMP_SCOPE StampScope _stamp_scope;
+// per-step roles of a multi-step kernel: flushed unless Args::stamp_skip (the PPO rollout keeps one step's)
+#define STAMP_SCOPE_A(A) StampScope _stamp_scope(!(A).stamp_skip);
 // Newton-phase accumulators (diag build): NT_MARK(ph) adds the cycles since the previous mark to phase ph
 #define NT_DECL unsigned long long _nt_acc[5] = {0, 0, 0, 0, 0}, _nt_last = 0;
 #define NT_NOW(v)                                                                \
@@ -84,6 +87,7 @@ struct StampScope {
 #define NT_MARK(ph)
 #define NT_FLUSH
 #define STAMP_SCOPE
+#define STAMP_SCOPE_A(A)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -164,6 +168,9 @@ struct Args {
   // the action alone) during step k from next_action into nctrl (LDS [3][64]); read when sm_in
   const float* next_action = nullptr;
   float* nctrl = nullptr;
+#ifdef AK_STAMPS
+  int stamp_skip = 0;  // diagnostic build: this role call's stamps are not flushed
+#endif
 };
 
 // Args of step k of a rollout launch: the k-th action row and, with per_step, the k-th output slices

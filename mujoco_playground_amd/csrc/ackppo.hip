@@ -268,6 +268,7 @@ struct GradArgs {
   float scale, max_norm, b1, b2, eps, step_size, bc2_sqrt;
   float* norm_out;
   float lsmin;  // opt-in log_std floor (ackppo_train_desc::log_std_min; -inf: none)
+  const float* wimg;  // ackppo_grad1i: the weight image (ackppo_train_desc::weight_image)
 };
 
 // ---- Adam (torch.optim.Adam after clip_grad_norm_), shared by ackppo_adam_kernel and the update
@@ -281,10 +282,17 @@ struct AdamK {
 __device__ __forceinline__ float grad_norm256(const float* __restrict__ g, float scale, float* red) {
   static_assert(P % 4 == 0, "float4 parameter vector");
   const int tid = threadIdx.x;
+  constexpr int NJ = (P / 4 + 255) / 256;
+  float4 v[NJ];  // every load in flight at once (a rolled loop waited for each L2 round trip in turn)
+#pragma unroll
+  for (int i = 0; i < NJ; i++) {
+    const int j = tid + 256 * i;
+    v[i] = j < P / 4 ? reinterpret_cast<const float4*>(g)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float ss = 0.0f;
-  for (int j = tid; j < P / 4; j += 256) {
-    const float4 v = reinterpret_cast<const float4*>(g)[j];
-    const float x = v.x * scale, y = v.y * scale, z = v.z * scale, w = v.w * scale;
+#pragma unroll
+  for (int i = 0; i < NJ; i++) {
+    const float x = v[i].x * scale, y = v[i].y * scale, z = v[i].z * scale, w = v[i].w * scale;
     ss = fmaf(x, x, ss);
     ss = fmaf(y, y, ss);
     ss = fmaf(z, z, ss);
@@ -414,11 +422,51 @@ constexpr int HB = HW + 2 * H;        // actor: b[2], log_std[2] (critic: b[1])
 constexpr int WEND = HB + 4;
 constexpr int X = WEND, H1 = X + 80 * LDP, H2 = H1 + H * LDP, D2 = H2 + H * LDP;  // D1 overwrites H1
 constexpr int GA = D2 + H * LDP;      // actor: gmu [2][LDP], glog [2][LDP]; critic: gv [LDP]
-constexpr int TOTAL = GA + 4 * LDP;
-static_assert(TOTAL * 4 * 2 <= 160 * 1024, "two one-net grad workgroups must share a CU's 160 KiB LDS");
+constexpr int TOTAL1 = GA + 4 * LDP;
+constexpr int TSZ = TOTAL1 - WEND;  // one tile's region (X .. GA)
+// NT tiles per workgroup (AK_GRAD1_NT): 1 = 256 threads, two workgroups per CU; 2 = 512 threads,
+// the two tiles' waves share one staged copy of the net's weights and one partial row (half the
+// rows for ackppo_reduce), one workgroup per CU
+#ifndef AK_GRAD1_NT
+#define AK_GRAD1_NT 2
+#endif
+#ifndef AK_GRAD1_PREFETCH
+#define AK_GRAD1_PREFETCH 0
+#endif
+constexpr int NT = AK_GRAD1_NT;
+static_assert(NT == 1 || NT == 2, "one or two tiles per workgroup");
+constexpr int TOTAL = WEND + NT * TSZ;
+static_assert(NT == 2 ? TOTAL * 4 <= 160 * 1024 : TOTAL * 4 * 2 <= 160 * 1024,
+              "two one-net grad workgroups (or one two-tile workgroup) per CU's 160 KiB LDS");
+// NT == 2: the end-of-kernel exchange of the halves' accumulators fits a tile region
+static_assert(22 * 256 <= TSZ && 16 * 256 <= TSZ, "accumulator exchange");
 __device__ __forceinline__ int w1t(int k, int u) { return W1T + k * H + (u ^ (16 * (k & 3)) ^ ((k >> 2) & 15)); }
 __device__ __forceinline__ int w2(int u, int k) { return W2 + w2_at(u, k); }
 constexpr int MAX_TILES = GRAD_MAX_BLOCKS;  // partial rows: one per tile (both nets' workgroups write it)
+// the weight image (ackppo_train_desc::weight_image): net n's LDS weight block [0, WEND) at
+// n * WIMG, padded to whole 64-lane rounds of float4 copies
+constexpr int WIMG = ACKPPO_WIMAGE;
+static_assert(WEND <= WIMG && WIMG % 256 == 0 && WIMG - WEND < 256, "weight image: WEND in whole 64-lane float4 rounds");
+static_assert(WIMG <= TOTAL, "the image copy's padding lands inside the workgroup's LDS");
+// image position of parameter p (-1: a pad word); the inverse of stage_net's LDS map
+__device__ __forceinline__ int wimg_index(int p) {
+  constexpr int NW1 = H * NOBS, NW2 = H * H;
+  if (p < ACKPPO_OFF_PI_W1) return p < 2 ? HB + 2 + p : -1;  // log_std
+  if (p >= ACKPPO_OFF_ACT_W) {
+    if (p < ACKPPO_OFF_ACT_B) return HW + (p - ACKPPO_OFF_ACT_W);
+    if (p < ACKPPO_OFF_ACT_B + 2) return HB + (p - ACKPPO_OFF_ACT_B);
+    if (p < ACKPPO_OFF_VAL_W) return -1;
+    if (p < ACKPPO_OFF_VAL_B) return WIMG + HW + (p - ACKPPO_OFF_VAL_W);
+    return p == ACKPPO_OFF_VAL_B ? WIMG + HB : -1;
+  }
+  const int net = p >= ACKPPO_OFF_VF_W1 ? 1 : 0;
+  const int r = p - (net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1);  // within [W1][b1][W2][b2]
+  const int base = net * WIMG;
+  if (r < NW1) return base + w1t(r % NOBS, r / NOBS);
+  if (r < NW1 + H) return base + B1 + (r - NW1);
+  if (r < NW1 + H + NW2) return base + w2((r - NW1 - H) / H, (r - NW1 - H) % H);
+  return base + B2 + (r - NW1 - H - NW2);
+}
 }  // namespace g1
 #ifndef AK_PPO_GRAD2
 #define AK_PPO_GRAD2 0
@@ -510,22 +558,23 @@ struct L2 {
   }
   static constexpr int B1 = g2::B1, B2 = g2::B2, HW = g2::HW, HB = g2::HB;
 };
-template <bool UPD, class LY = L1>
+template <bool UPD, class LY = L1, int NTHR = GRAD_THREADS>
 __device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, float* w, int net, int row, int nrow) {
   // all global loads first (one latency), then the LDS writes: W1 (float4 rows of 79 inputs)
   // transposed and swizzled, W2 swizzled, the short vectors
-  constexpr int N1 = H * NOBS / 4, IT1 = (N1 + GRAD_THREADS - 1) / GRAD_THREADS, IT2 = H * H / 4 / GRAD_THREADS;
+  constexpr int N1 = H * NOBS / 4, IT1 = (N1 + NTHR - 1) / NTHR, IT2 = H * H / 4 / NTHR;
+  static_assert(H * H / 4 % NTHR == 0, "whole W2 float4 rounds");
   const int tid = threadIdx.x;
   const int o1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, o2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
   float4 v[IT1], v2[IT2];
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
-    const int i = tid + j * GRAD_THREADS;
+    const int i = tid + j * NTHR;
     if (i < N1) stage_w4<UPD>(A, k, o1, i, row, nrow, v[j]);
   }
   if constexpr (UPD) __builtin_amdgcn_sched_barrier(0);  // W1's four arrays, then W2's: bounded registers
 #pragma unroll
-  for (int j = 0; j < IT2; j++) stage_w4<UPD>(A, k, o2, tid + j * GRAD_THREADS, row, nrow, v2[j]);
+  for (int j = 0; j < IT2; j++) stage_w4<UPD>(A, k, o2, tid + j * NTHR, row, nrow, v2[j]);
   __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the scatter (one memory latency)
   // short vectors: threads 0-63 b1, b2 and the head rows; 64-67 the head biases / log_std
   float b1 = 0.f, b2 = 0.f, hw0 = 0.f, hw1 = 0.f, hs = 0.f;
@@ -542,7 +591,7 @@ __device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, flo
                        row, nrow);
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
-    const int i = tid + j * GRAD_THREADS;
+    const int i = tid + j * NTHR;
     if (i < N1) {
       const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
@@ -555,7 +604,7 @@ __device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, flo
   if (tid < H) LY::w1(w, tid, NOBS, 0.0f);  // input 79: the zero pad of the 80-deep layer-1 product
 #pragma unroll
   for (int j = 0; j < IT2; j++) {
-    const int i = 4 * (tid + j * GRAD_THREADS), u = i / H, kk = i - u * H;
+    const int i = 4 * (tid + j * NTHR), u = i / H, kk = i - u * H;
     const float e[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w};
 #pragma unroll
     for (int c = 0; c < 4; c++) LY::w2(w, u, kk + c, e[c]);
@@ -567,6 +616,34 @@ __device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, flo
     w[LY::HW + H + tid] = hw1;
   }
   if (has_sc) w[LY::HB + sc] = hs;
+}
+
+// ackppo_grad1i's staging: the net's weight image copied into LDS by LDS-DMA (global_load_lds,
+// 16 B per lane: lane l of a wave writes float4 (base + l), the image already in the LDS layout) --
+// no registers, no transposing writes. The copies land behind the tile loop's first barrier.
+template <int NTHR>
+__device__ __forceinline__ void stage_image(const float* __restrict__ img, float* w) {
+  constexpr int N4 = g1::WIMG / 4;
+  static_assert(N4 % 64 == 0, "whole 64-lane rounds");
+  const int tid = threadIdx.x, wbase = tid & ~63;
+#pragma unroll
+  for (int j = 0; j < (N4 + NTHR - 1) / NTHR; j++) {
+    const int i0 = j * NTHR + wbase;  // wave-uniform: the round's LDS base
+    if (i0 < N4)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(img + 4 * (i0 + (tid & 63))),
+                                       (__attribute__((address_space(3))) void*)(w + 4 * i0), 16, 0, 0);
+  }
+}
+// the weight image of both nets from the parameters (once per ackppo_train call; every Adam step
+// then keeps it in step): stage_net's LDS map, written to HBM, pad words zero
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_wimage_kernel(const float* params, float* img) {
+  const int net = blockIdx.x;
+  float* w = img + net * g1::WIMG;
+  for (int i = threadIdx.x; i < g1::WIMG; i += GRAD_THREADS) w[i] = 0.0f;
+  __syncthreads();
+  GradArgs A{};
+  A.params = params;
+  stage_net<false, L1>(A, AdamK{}, w, net, 0, 1);
 }
 
 __device__ __forceinline__ float row_sum_t(const float* a) {  // 32 samples of one LDS tile row
@@ -616,18 +693,22 @@ __device__ __forceinline__ int vec_offset_g1(int net, int i) {
   return i < 192 ? ACKPPO_OFF_VAL_W + (i - 128) : ACKPPO_OFF_VAL_B;
 }
 
-template <bool UPD>
+template <bool UPD, bool IMG = false>
 __device__ __forceinline__ void grad1(const GradArgs& A) {
   using namespace g1;
   PRSTAMP(13);
   PSTAMP(0);
   extern __shared__ float tl[];
+  constexpr int NTHR = GRAD_THREADS * NT;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int net = blockIdx.x & 1, tile0 = blockIdx.x >> 1, tstride = gridDim.x >> 1;
+  // NT == 2: waves 0-3 take tile 2 g of tile group g, waves 4-7 tile 2 g + 1 (half = 1); htid is
+  // the thread's index within its half (every per-tile role below is the 256-thread one)
+  const int wave8 = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = NT == 1 ? 0 : wave8 >> 2, wave = wave8 & 3, htid = tid & (GRAD_THREADS - 1);
+  const int net = blockIdx.x & 1, grp0 = blockIdx.x >> 1, gstride = gridDim.x >> 1;
   float* w = tl;
   const float invB = 1.0f / (float)A.batch;
-  const int ntiles = (A.batch + T - 1) / T;
+  const int ntiles = (A.batch + T - 1) / T, ngrp = (ntiles + NT - 1) / NT;
   const int li = lane & 15, lk = lane >> 4;
   const int ub = 16 * wave;  // the wave's unit tile
   // heads' lane roles: wave w, samples 8 w + (lane & 7); actor lanes (d = (lane >> 3) & 1, quarter
@@ -637,17 +718,18 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   auto loads = [&](int tile) __attribute__((always_inline)) {
     // unconditional loads from valid addresses (a clamped sample and input), zeros selected after:
-    // conditional loads compile to exec-masked branches that wait for each load in turn
-    const int s0 = tile * T, nvalid = min(T, A.batch - s0);
-    const int r = tid >> 3, q = tid & 7;
-    const float* row = A.obs_rows + (size_t)A.idx[s0 + min(r, nvalid - 1)] * NOBS;
+    // conditional loads compile to exec-masked branches that wait for each load in turn. A tile
+    // past the batch (the second half of a last, odd group) has nvalid = 0: sample 0's rows, all zeroed
+    const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
+    const int r = htid >> 3, q = htid & 7;
+    const float* row = A.obs_rows + (size_t)A.idx[nvalid > 0 ? s0 + min(r, nvalid - 1) : 0] * NOBS;
 #pragma unroll
     for (int i = 0; i < 10; i++) {
       const int k = q * 10 + i;
       const float v = row[min(k, NOBS - 1)];
       xg[i] = (r < nvalid && k < NOBS) ? v : 0.0f;
     }
-    const int sidx = A.idx[s0 + min(hs, nvalid - 1)];
+    const int sidx = A.idx[nvalid > 0 ? s0 + min(hs, nvalid - 1) : 0];
     const bool hv = hs < nvalid;
     if (net == 0) {
       const float2 a = *reinterpret_cast<const float2*>(A.actions + 2 * (size_t)sidx);
@@ -662,14 +744,17 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     }
   };
 
-  if (tile0 < ntiles) loads(tile0);
+  // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
+  // overlaps it; the registers they hold through the staging cost a few spill slots)
+  if (AK_GRAD1_PREFETCH && grp0 < ngrp) loads(NT * grp0 + half);
   AdamK ak{};
   if constexpr (UPD) {  // the pending Adam step: the global norm first (every workgroup, same order)
     const float norm = grad_norm256(A.upd, A.scale, tl + X);
     ak = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
     if (blockIdx.x == 0 && tid == 0 && A.norm_out) A.norm_out[0] = norm;
   }
-  stage_net<UPD>(A, ak, w, net, tile0, tstride);
+  if constexpr (IMG) stage_image<NTHR>(A.wimg + net * WIMG, w);
+  else stage_net<UPD, L1, NTHR>(A, ak, w, net, grp0, gstride);
 
   f4v gw1[5], gw2[4];
 #pragma unroll
@@ -679,18 +764,19 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   float accv[2] = {0.0f, 0.0f};  // vector items tid and tid + 256 (vec_item_g1)
   float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;
 
-  for (int tile = tile0; tile < ntiles; tile += tstride) {
+  for (int grp = grp0; grp < ngrp; grp += gstride) {  // the same trip count in both halves (barriers)
+    const int tile = NT * grp + half;
     // an opaque zero per tile: every LDS address below depends on it, so none is hoisted out of the
     // tile loop (the hoisted swizzled addresses filled the register file and spilled)
     int zo = 0;
     asm volatile("" : "+v"(zo));
-    float* tb = tl + zo;
-    const float* wb = tb;
-    const int s0 = tile * T, nvalid = min(T, A.batch - s0);
+    float* tb = tl + zo + half * TSZ;
+    const float* wb = tl + zo;
+    const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
     __syncthreads();  // the previous tile's LDS reads are done (and the weights staged)
-    if (tile != tile0) loads(tile);
+    if (!AK_GRAD1_PREFETCH || grp != grp0) loads(tile);
     {
-      const int r = tid >> 3, q = tid & 7;
+      const int r = htid >> 3, q = htid & 7;
 #pragma unroll
       for (int i = 0; i < 10; i++) tb[X + (q * 10 + i) * LDP + r] = xg[i];
     }
@@ -794,7 +880,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     __syncthreads();
     PSTAMP(4);
     {  // D2 = dL/dH2 (1 - H2^2): thread (unit tid >> 2, samples 8 (tid & 3) ...)
-      const int u = tid >> 2, c0 = 8 * (tid & 3);
+      const int u = htid >> 2, c0 = 8 * (htid & 3);
       const float ha = wb[HW + u], hb = net ? 0.0f : wb[HW + H + u];
 #pragma unroll
       for (int c = c0; c < c0 + 8; c += 4) {
@@ -836,7 +922,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     // vector items read before D1 replaces H1 (vec_item_g1): b2 and the heads
 #pragma unroll
     for (int bb = 0; bb < 2; bb++) {
-      const int i = tid + bb * GRAD_THREADS;
+      const int i = htid + bb * GRAD_THREADS;
       if (i >= 64 && i < (net ? G1_NVC : G1_NVA)) accv[bb] += vec_item_g1(tb, net, i);
     }
     __syncthreads();  // every read of H1 (gW2) and H2 is done: D1 may replace H1
@@ -859,28 +945,72 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       for (int j = 0; j < 5; j++) gw1[j] = mfma4(a, tb[X + (16 * j + li) * LDP + q], gw1[j]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (tid < H) accv[0] += vec_item_g1(tb, net, tid);
+    if (htid < H) accv[0] += vec_item_g1(tb, net, htid);
   }
   PSTAMP(8);
-  // this workgroup's half of partial row tile0: its net's weight gradients and vector items
-  const int row = tile0;
+  // this workgroup's net's share of partial row grp0: its weight gradients and vector items
+  const int row = grp0;
   float* g = A.gpart + (size_t)row * P;
-  {
-    const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
+  const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
+  bool st_w1 = true, st_w2 = true;
+  if constexpr (NT == 2) {
+    // the halves' sums combined through LDS, tile 2 g's first: half 1 hands over gW1 and the vector
+    // items (into its tile region) and stores the combined gW2; half 0 hands over gW2 and stores
+    // the combined gW1 and vector items
+    __syncthreads();  // every tile read is done
+    float* xo = tl + WEND + half * TSZ;  // this half's hand-over region, [component][256]
+    const float* xi = tl + WEND + (1 - half) * TSZ;
+    if (half == 1) {
+#pragma unroll
+      for (int j = 0; j < 5; j++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) xo[(4 * j + r) * GRAD_THREADS + htid] = gw1[j][r];
+      xo[20 * GRAD_THREADS + htid] = accv[0];
+      xo[21 * GRAD_THREADS + htid] = accv[1];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) xo[(4 * j + r) * GRAD_THREADS + htid] = gw2[j][r];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int j = 0; j < 5; j++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) gw1[j][r] = gw1[j][r] + xi[(4 * j + r) * GRAD_THREADS + htid];
+      accv[0] = accv[0] + xi[20 * GRAD_THREADS + htid];
+      accv[1] = accv[1] + xi[21 * GRAD_THREADS + htid];
+      st_w2 = false;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) gw2[j][r] = xi[(4 * j + r) * GRAD_THREADS + htid] + gw2[j][r];
+      st_w1 = false;
+    }
+  }
+  if (st_w1) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int u = ub + 4 * lk + r;
 #pragma unroll
       for (int j = 0; j < 5; j++)
         if (16 * j + li < NOBS) g[ow1 + u * NOBS + 16 * j + li] = gw1[j][r];
+    }
+#pragma unroll
+    for (int bb = 0; bb < 2; bb++) {
+      const int i = htid + bb * GRAD_THREADS;
+      if (i < (net ? G1_NVC : G1_NVA)) g[vec_offset_g1(net, i)] = accv[bb];
+    }
+  }
+  if (st_w2) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int u = ub + 4 * lk + r;
 #pragma unroll
       for (int j = 0; j < 4; j++) g[ow2 + u * H + 16 * j + li] = gw2[j][r];
     }
-  }
-#pragma unroll
-  for (int bb = 0; bb < 2; bb++) {
-    const int i = tid + bb * GRAD_THREADS;
-    if (i < (net ? G1_NVC : G1_NVA)) g[vec_offset_g1(net, i)] = accv[bb];
   }
   // loss sums: per wave, then the four waves in order through LDS (the tile is done)
   la = wave_sum(la);
@@ -889,14 +1019,15 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   ln = wave_sum(ln);
   __syncthreads();
   if (lane == 0) {
-    tl[X + 4 * wave + 0] = la;
-    tl[X + 4 * wave + 1] = lb;
-    tl[X + 4 * wave + 2] = lc;
-    tl[X + 4 * wave + 3] = ln;
+    tl[X + 4 * wave8 + 0] = la;
+    tl[X + 4 * wave8 + 1] = lb;
+    tl[X + 4 * wave8 + 2] = lc;
+    tl[X + 4 * wave8 + 3] = ln;
   }
   __syncthreads();
   if (tid < 4) {
-    const float s = (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]);
+    float s = (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]);
+    if constexpr (NT == 2) s = s + ((tl[X + 16 + tid] + tl[X + 20 + tid]) + (tl[X + 24 + tid] + tl[X + 28 + tid]));
     float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
     if (net == 0) {
       lp[tid == 0 ? 0 : tid + 1] = s;  // policy loss, clipped count, approx-kl sum, samples
@@ -908,8 +1039,15 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   PSTAMP(15);
   PRSTAMP(14);
 }
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1_kernel(GradArgs A) { grad1<false>(A); }
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 2) ackppo_grad1u_kernel(GradArgs A) { grad1<true>(A); }
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1_kernel(GradArgs A) {
+  grad1<false>(A);
+}
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1u_kernel(GradArgs A) {
+  grad1<true>(A);
+}
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1i_kernel(GradArgs A) {
+  grad1<false, true>(A);
+}
 
 // ---- ackppo_grad, one net per workgroup, 16 samples per WAVE (default, AK_PPO_GRAD2). Workgroup
 // 2 t + net takes the actor (net 0) or the critic (net 1) of 64-sample tile t; wave w carries samples
@@ -1428,48 +1566,78 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int 
 // (row by belongs to group by alone, and element (by, p) to one thread, which read it first);
 // (2) sums rows 0..RG-1. The caller-owned partial rows are the only buffer, so concurrent
 // learners on other streams or devices share nothing.
-// One-launch reduction (default): a 1024-thread block owns 64 consecutive parameters; its 16
-// waves each sum every 16th partial row of them (coalesced 256-byte row reads, four loads in
-// flight per lane), the 16 sums are combined through LDS; block 0 also reduces the loss rows.
+// One-launch reduction (default): a 1024-thread block owns 64 x R1_V consecutive parameters; its
+// 16 waves each sum every 16th partial row of them (coalesced 1 KB row reads at R1_V = 4, every
+// row load in flight at once), the 16 sums are combined through LDS; block 0 also reduces the loss
+// rows. At R1_V = 4 the 18 764 parameters take 74 blocks (R1_V = 1: 294, more than one per CU).
 // It replaced the two-launch form below (row groups in place, then the group sums).
 #ifndef AK_PPO_REDUCE1
 #define AK_PPO_REDUCE1 1
 #endif
-constexpr int R1_P = 64, R1_G = 16;
+#ifndef AK_PPO_R1VEC  // parameters per lane of the one-launch reduction (1, 2 or 4: float, float2, float4 loads)
+#define AK_PPO_R1VEC 1
+#endif
+constexpr int R1_P = 64, R1_G = 16, R1_V = AK_PPO_R1VEC, R1_PB = R1_P * R1_V;  // R1_PB parameters per block
+static_assert(P % R1_V == 0, "whole vectors per partial row");
+template <int V>
+struct R1Vec;
+template <>
+struct R1Vec<1> {
+  using T = float;
+  static __device__ __forceinline__ float at(const T& v, int) { return v; }
+};
+template <>
+struct R1Vec<2> {
+  using T = float2;
+  static __device__ __forceinline__ float at(const T& v, int c) { return c ? v.y : v.x; }
+};
+template <>
+struct R1Vec<4> {
+  using T = float4;
+  static __device__ __forceinline__ float at(const T& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
+};
 extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce1_kernel(const float* gpart, int nblk,
                                                                         const float* lpart, float ent_coef,
                                                                         float* grad, float* loss, int accumulate) {
-  __shared__ float red[R1_G][R1_P + 1];
+  // a block owns R1_PB consecutive parameters: lane pl of wave g loads R1_V of them (one vector
+  // load per partial row: 64 lanes x 4 floats = a 1 KB coalesced read) from every 16th row
+  using VT = typename R1Vec<R1_V>::T;
+  __shared__ float red[R1_G][R1_PB + 1];
   __shared__ float lred[256];
   const int tid = threadIdx.x, pl = tid & (R1_P - 1), g = tid / R1_P;
-  const int pidx = blockIdx.x * R1_P + pl;
+  const int vidx = blockIdx.x * R1_P + pl;  // vector index
+  const bool vok = vidx < P / R1_V;
   // all R1_K of this thread's rows in flight at once (one memory latency, not four), then summed in
   // the order of the original loop -- blocks of 4 rows into acc[0..3] while a whole block of 4
-  // remains, the tail rows into acc[0] -- so the result is the same, bit for bit
+  // remains, the tail rows into acc[0] -- per parameter the same order whatever R1_V is
   constexpr int R1_K = GRAD_MAX_BLOCKS / R1_G;
   static_assert(R1_K % 4 == 0, "row blocks of four");
-  float x[R1_K];
+  VT x[R1_K];
 #pragma unroll
   for (int k = 0; k < R1_K; k++) {
     const int b = g + k * R1_G;
-    x[k] = (pidx < P && b < nblk) ? gpart[(size_t)b * P + pidx] : 0.0f;
+    x[k] = (vok && b < nblk) ? reinterpret_cast<const VT*>(gpart + (size_t)b * P)[vidx] : VT{};
   }
   int nmain = 0;  // blocks j with g + 4 R1_G j + 3 R1_G < nblk (a prefix)
 #pragma unroll
   for (int j = 0; j < R1_K / 4; j++) nmain += (g + 4 * R1_G * j + 3 * R1_G < nblk) ? 1 : 0;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < R1_K / 4; j++)
-    if (j < nmain) {
+  for (int c = 0; c < R1_V; c++) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
-    }
+    for (int j = 0; j < R1_K / 4; j++)
+      if (j < nmain) {
 #pragma unroll
-  for (int k = 0; k < R1_K; k++)
-    if (k >= 4 * nmain) acc[0] += x[k];  // rows past nblk are 0.0f: adding them changes nothing
-  red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        for (int i = 0; i < 4; i++) acc[i] += R1Vec<R1_V>::at(x[4 * j + i], c);
+      }
+#pragma unroll
+    for (int k = 0; k < R1_K; k++)
+      if (k >= 4 * nmain) acc[0] += R1Vec<R1_V>::at(x[k], c);  // rows past nblk are 0.0f: adding them changes nothing
+    red[g][R1_V * pl + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
   __syncthreads();
-  if (tid < R1_P && pidx < P) {
+  const int pidx = blockIdx.x * R1_PB + tid;
+  if (tid < R1_PB && pidx < P) {
     float s = 0.0f;
 #pragma unroll
     for (int k = 0; k < R1_G; k++) s += red[k][tid];
@@ -1541,15 +1709,19 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
 extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* params, const float* grad, float* m,
                                                                      float* v, float scale, float max_norm, float b1,
                                                                      float b2, float eps, float step_size,
-                                                                     float bc2_sqrt, float* norm_out, float lsmin) {
+                                                                     float bc2_sqrt, float* norm_out, float lsmin,
+                                                                     float* wimg) {
   __shared__ float red[4];
+  // this thread's parameter and moments are loaded before the norm (their latency hides under it)
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int jc = j < P / 4 ? j : P / 4 - 1;
+  const float4 pv = reinterpret_cast<const float4*>(params)[jc];
+  const float4 mv = reinterpret_cast<const float4*>(m)[jc], vv = reinterpret_cast<const float4*>(v)[jc];
   const float norm = grad_norm256(grad, scale, red);
   const AdamK k = adam_k(norm, scale, max_norm, b1, b2, eps, step_size, bc2_sqrt, lsmin);
   if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
-  const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= P / 4) return;
-  const float4 pv = reinterpret_cast<const float4*>(params)[j], gv = reinterpret_cast<const float4*>(grad)[j];
-  const float4 mv = reinterpret_cast<const float4*>(m)[j], vv = reinterpret_cast<const float4*>(v)[j];
+  const float4 gv = reinterpret_cast<const float4*>(grad)[j];
   float4 pn, mn, vn;
   adam_elem(k, pv.x, gv.x, mv.x, vv.x, pn.x, mn.x, vn.x);
   adam_elem(k, pv.y, gv.y, mv.y, vv.y, pn.y, mn.y, vn.y);
@@ -1563,6 +1735,14 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* para
   reinterpret_cast<float4*>(params)[j] = pn;
   reinterpret_cast<float4*>(m)[j] = mn;
   reinterpret_cast<float4*>(v)[j] = vn;
+  if (wimg) {  // the new parameters into the weight image as well (ackppo_grad1i stages from it)
+    const float o[4] = {pn.x, pn.y, pn.z, pn.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int ix = g1::wimg_index(4 * j + c);
+      if (ix >= 0) wimg[ix] = o[c];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ C-ABI
@@ -1604,16 +1784,18 @@ bool policy_lds_ready() {
   return true;
 }
 bool g_grad1u_attr[MAX_DEV] = {};
+bool g_grad1i_attr[MAX_DEV] = {};
 // ackppo_grad's launch: two workgroups (actor, critic) per partial row; with A.upd, the variant that
 // applies the pending Adam step while staging (ackppo_train)
 int grad_launch(const GradArgs& A, void* stream) {
   const int dev = current_device();
   if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
-  const bool upd = A.upd != nullptr;
-  bool& ready = upd ? g_grad1u_attr[dev] : g_grad_attr[dev];
+  const bool upd = A.upd != nullptr, img = !upd && A.wimg != nullptr && !AK_PPO_GRAD2;
+  bool& ready = upd ? g_grad1u_attr[dev] : (img ? g_grad1i_attr[dev] : g_grad_attr[dev]);
   if (!ready) {
     const void* kern = AK_PPO_GRAD2 ? (upd ? (const void*)ackppo_grad2u_kernel : (const void*)ackppo_grad2_kernel)
-                                    : (upd ? (const void*)ackppo_grad1u_kernel : (const void*)ackppo_grad1_kernel);
+                                    : (upd ? (const void*)ackppo_grad1u_kernel
+                                           : (img ? (const void*)ackppo_grad1i_kernel : (const void*)ackppo_grad1_kernel));
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS) != hipSuccess)
       return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
     ready = true;
@@ -1623,7 +1805,8 @@ int grad_launch(const GradArgs& A, void* stream) {
     hipLaunchKernelGGL(upd ? ackppo_grad2u_kernel : ackppo_grad2_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
                        GRAD_LDS, (hipStream_t)stream, A);
   else
-    hipLaunchKernelGGL(upd ? ackppo_grad1u_kernel : ackppo_grad1_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
+    hipLaunchKernelGGL(upd ? ackppo_grad1u_kernel : (img ? ackppo_grad1i_kernel : ackppo_grad1_kernel), dim3(2 * nblk),
+                       dim3(GRAD_THREADS * g1::NT),
                        GRAD_LDS, (hipStream_t)stream, A);
   return launched("ackppo_grad");
 }
@@ -1773,14 +1956,15 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
 int ackppo_grad_blocks(int batch) {
   if (batch <= 0) return 0;
   const int tiles = (batch + (AK_PPO_GRAD2 ? g2::T : g1::T) - 1) / (AK_PPO_GRAD2 ? g2::T : g1::T);
-  return tiles < GRAD_MAX_BLOCKS ? tiles : GRAD_MAX_BLOCKS;
+  const int rows = AK_PPO_GRAD2 ? tiles : (tiles + g1::NT - 1) / g1::NT;  // one partial row per tile group
+  return rows < GRAD_MAX_BLOCKS ? rows : GRAD_MAX_BLOCKS;
 }
 
 namespace {
 int reduce_launch(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, int accumulate, void* stream) {
   if (AK_PPO_REDUCE1) {
-    hipLaunchKernelGGL(ackppo_reduce1_kernel, dim3((P + R1_P - 1) / R1_P), dim3(R1_P * R1_G), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(ackppo_reduce1_kernel, dim3((P + R1_PB - 1) / R1_PB), dim3(R1_P * R1_G), 0, (hipStream_t)stream,
                        grad_partial, nblk, loss_partial, ent_coef, grad, loss, accumulate);
     return launched("ackppo_reduce");
   }
@@ -1803,11 +1987,11 @@ int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, floa
 namespace {
 int adam_launch(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
                 float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
-                float* grad_norm_out, float lsmin, void* stream) {
+                float* grad_norm_out, float lsmin, void* stream, float* wimg = nullptr) {
   if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(ACKPPO_EINVAL, "ackppo_adam: bad arguments");
   hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P / 4 + 255) / 256), dim3(256), 0, (hipStream_t)stream, params, grad,
                      exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
-                     grad_norm_out, lsmin);
+                     grad_norm_out, lsmin, wimg);
   return launched("ackppo_adam");
 }
 }  // namespace
@@ -1858,11 +2042,16 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
   if ((d->world > 1 && !dp) || (dp && !d->moments))
     return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
   const bool fuse = d->params2 && d->exp_avg2 && d->exp_avg_sq2;
+  float* wimg = (fuse || AK_PPO_GRAD2) ? nullptr : d->weight_image;
   const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
     return fail(ACKPPO_EHIP, "ackppo_train: hipMemsetAsync(loss_acc)");
   if (S == 0 || d->n_epochs == 0) return ACKPPO_OK;
+  if (wimg) {  // the image of the parameters as they are now; each Adam step below keeps it current
+    hipLaunchKernelGGL(ackppo_wimage_kernel, dim3(2), dim3(GRAD_THREADS), 0, st, d->params, wimg);
+    if (const int rc0 = launched("ackppo_train: weight image")) return rc0;
+  }
   const float scale = 1.0f / (float)d->world;
   int rc;
   auto coll = [&](void* buf, int64_t count, int dtype, const char* what) -> int {
@@ -1903,6 +2092,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
       const int nb = S - m * B < B ? S - m * B : B;
       GradArgs A{pv[cur], d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, d->perm + (size_t)m * B, nb,
                  d->stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial};
+      A.wimg = wimg;
       if (pending) {  // fused: the previous minibatch's Adam step, applied while this launch stages
         A.upd = d->grad;
         A.m_in = mv[cur];
@@ -1932,7 +2122,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
         float ss, bc2;
         adam_scalars(t, ss, bc2);
         if ((rc = adam_launch(pv[cur], d->grad, mv[cur], vv[cur], scale, d->max_grad_norm, (float)d->beta1,
-                              (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream)))
+                              (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream, wimg)))
           return rc;
       }
     }

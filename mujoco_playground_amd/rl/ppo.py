@@ -167,6 +167,8 @@ class PPO:
         self.grad = torch.zeros(NPARAM, **f32)
         # the alternate parameter / moment vectors of the fused Adam step (ackppo_train_desc params2 ...)
         self.scratch = torch.zeros(3, NPARAM, **f32)
+        # both nets' gradient-kernel weight blocks in the kernel's LDS layout (ackppo_train_desc weight_image)
+        self.weight_image = torch.zeros(2 * _lib.ACKPPO_WIMAGE, **f32)
         self.loss = torch.zeros(NLOSS, **f32)
         self.loss_acc = torch.zeros(NLOSS, **f32)
         self.gnorm = torch.zeros(1, **f32)
@@ -298,7 +300,18 @@ class PPO:
         d.world = self.world
         d.log_std_min = float("-inf") if self.log_std_min is None else float(self.log_std_min)
         self.set_fuse_adam(False, d)
+        self.set_weight_image(False, d)
         return d
+
+    def set_weight_image(self, on: bool, d=None):
+        """on: the gradient launches copy each net's weights into LDS from a pre-laid-out image that
+        every Adam step keeps current (ackppo_train_desc weight_image; the same bits); off (default):
+        they transpose the parameter vector themselves. Measured (profiles/r04l_ppo_timing.log, the
+        two-tile gradient workgroups): 32.5 us per minibatch with the image against 32.1 without --
+        the gradient launch gains 0.4 us (21.07 -> 20.71), the Adam launch's scatter into the image
+        costs as much (4.99 -> 5.34)."""
+        d = self._desc if d is None else d
+        d.weight_image = self.weight_image.data_ptr() if on else None
 
     def set_fuse_adam(self, on: bool, d=None):
         """on: each minibatch's Adam step applied by the next gradient launch while it stages the

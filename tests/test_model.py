@@ -138,3 +138,11 @@ def test_ctypes_structs_match_the_c_layouts(tmp_path):
         assert int(got[f"{cname} size"]) == C.sizeof(py), cname
         for f, _t in py._fields_:
             assert int(got[f"{cname} {f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def test_weight_image_size_matches_the_header():
+    """_lib.ACKPPO_WIMAGE (the PPO learner's weight-image buffer, floats per net) = include/ackppo.h."""
+    import re
+    with open(os.path.join(_lib.REPO, "include", "ackppo.h")) as f:
+        m = re.search(r"#define ACKPPO_WIMAGE (\d+)", f.read())
+    assert m and int(m.group(1)) == _lib.ACKPPO_WIMAGE

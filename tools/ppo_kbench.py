@@ -59,7 +59,9 @@ def run(path):
         e1.record()
         torch.cuda.synchronize()
         res[name] = round(e0.elapsed_time(e1) / 20 * 1000, 1)
-    print(path, res, "grad checksum", float(grad.abs().sum()), flush=True)
+    import hashlib
+    print(path, res, "grad checksum", float(grad.abs().sum()), "grad sha1",
+          hashlib.sha1(grad.cpu().numpy().tobytes()).hexdigest()[:12], flush=True)
 
 
 if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "--stamps"):

@@ -1,9 +1,11 @@
 """Where a PPO update's time goes: one rollout (4096 envs x 32 steps), then PPO.train() timed with the
-Adam step fused into the gradient launch and on its own (event-timed, 3 calls each). Under
+Adam step fused into the gradient launch or on its own, with and without the weight image
+(event-timed, 3 calls each). Under
 `rocprofv3 --kernel-trace` (tools/gpu_r04f.sh) the kernel trace then gives each kernel's duration
 and the idle gaps between consecutive kernels (tools/probes/ppo_update_timeline.py --trace DIR).
 
     python tools/probes/ppo_update_timeline.py              (timing)
+    python tools/probes/ppo_update_timeline.py --only 0,1    (one configuration: fuse_adam, weight_image)
     python tools/probes/ppo_update_timeline.py --trace DIR  (summarise a rocprofv3 kernel trace)
 """
 import csv
@@ -15,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 
-def timing():
+def timing(configs=((False, True), (False, False), (True, False), (False, True), (False, False), (True, False))):
     import torch
     from mujoco_playground_amd.rl import AckermannVecEnv
     from mujoco_playground_amd.rl.ppo import PPO
@@ -24,8 +26,9 @@ def timing():
     model = PPO("MlpPolicy", venv, n_steps=32, batch_size=8192, n_epochs=10, seed=0)
     model.collect_rollouts()
     nmb = 32 * 4096 // 8192 * 10
-    for fuse in (False, True, False, True):
+    for fuse, img in configs:
         model.set_fuse_adam(fuse)
+        model.set_weight_image(img)
         model.train()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
@@ -35,7 +38,8 @@ def timing():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 3
-        print(f"fuse_adam={fuse}: train() {ms:.3f} ms = {ms * 1e3 / nmb:.2f} us per minibatch", flush=True)
+        print(f"fuse_adam={fuse} weight_image={img}: train() {ms:.3f} ms = {ms * 1e3 / nmb:.2f} us per minibatch",
+              flush=True)
 
 
 def trace(d):
@@ -63,5 +67,8 @@ def trace(d):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--trace":
         trace(sys.argv[2])
+    elif len(sys.argv) > 2 and sys.argv[1] == "--only":  # one configuration (for a kernel trace): FUSE,IMAGE
+        f, i = (bool(int(v)) for v in sys.argv[2].split(","))
+        timing(((f, i),))
     else:
         timing()

@@ -11,7 +11,8 @@ timed launch (the kernel's last dispatch) are divided by its K steps: bytes and 
 step. Entries are keyed "<kernel>@K<k>"; bench.py reports the entry whose K equals its --steps (or
 the nearest K, saying so), since a launch's first-step loads and last-step stores are spread over
 its K steps.
-    python3 tools/profile_pmc.py [K,K,...] [--buffers]   (default 20,1000: the driver's and bench's defaults)
+    python3 tools/profile_pmc.py [K,K,...] [--buffers] [--obstacles]   (default 20,1000: the driver's and bench's defaults)
+--obstacles: the obstacle scene's rollout kernel (bench.py --scene obstacles), -> pmc_latest_obst.json.
 --buffers: the same launches with per-step output slices (bench.py --buffers: a [K][79][N] rollout
 buffer), keyed "<kernel>@K<k>+buf" with per_step_outputs true.
 """
@@ -23,9 +24,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {0: "ackphys_rollout_nc_kernel", 1: "ackphys_rollout_quad_kernel"}
 ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
 BUFFERS = "--buffers" in sys.argv[1:]
+OBST = "--obstacles" in sys.argv[1:]  # the obstacle scene's rollout kernel (contacts on), keyed without a suffix
+KERNELS = {1: "ackphys_rollout_obst8_kernel"} if OBST else {0: "ackphys_rollout_nc_kernel", 1: "ackphys_rollout_quad_kernel"}
 KS = [int(k) for k in (ARGS[0] if ARGS else "20,1000").split(",")]
 
 
@@ -34,7 +36,7 @@ def run_pass(counters, out, contacts, k):
     cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o",
            "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
            "--no-obstacles", "--no-per-step", "--no-buffer-leg", "--steps", str(k), "--warmup", "5", "--contacts",
-           str(contacts)] + (["--buffers"] if BUFFERS else [])
+           str(contacts)] + (["--buffers"] if BUFFERS else []) + (["--scene", "obstacles"] if OBST else [])
     env = dict(os.environ, TMPDIR="/tmp")
     subprocess.run(cmd, check=True, cwd="/tmp", env=env, stdout=subprocess.DEVNULL)
     vals = {c: {} for c in counters}  # counter -> dispatch id -> value (summed over the rows of a dispatch)
@@ -51,7 +53,7 @@ def main():
     res = {}
     for k in KS:
         for contacts, kern in KERNELS.items():
-            out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}_k{k}{'_buf' if BUFFERS else ''}")
+            out = os.path.join(ROOT, "gpurun_out", f"pmc_c{contacts}_k{k}{'_buf' if BUFFERS else ''}{'_obst' if OBST else ''}")
             f = run_pass(["FETCH_SIZE"], out + "_fetch", contacts, k)["FETCH_SIZE"]
             w = run_pass(["WRITE_SIZE"], out + "_write", contacts, k)["WRITE_SIZE"]
             sq = run_pass(["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"], out + "_sq", contacts, k)
@@ -67,7 +69,8 @@ def main():
                 "valu_insts_per_wave_step": (sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] / k) if sq["SQ_WAVES"] else None,
             }
             print(json.dumps({key: res[key]}), flush=True)
-    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest" + ("_buf" if BUFFERS else "") + ".json"), "w"),
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_latest" + ("_buf" if BUFFERS else "") + ("_obst" if OBST else "")
+                        + ".json"), "w"),
               indent=1)
 
 

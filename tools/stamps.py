@@ -1,6 +1,8 @@
 """Per-phase cycle breakdown of ackphys_step_kernel from the stamped diagnostic build.
 
-    tools/build_diag.sh && python tools/stamps.py
+    tools/build_diag.sh && python tools/stamps.py [quad|obst]
+    (STAMPS_ROLLOUT=K: the last step of K-step ackphys_rollout launches; STAMPS_JSON=path: merge the
+    per-kernel summaries into that file, e.g. profiles/critical_path_latest.json)
 Phases (stamp k -> k+1): 0 load/controller, 1 kinematics->dynamics entry, 2 M/bias/a0,
 3 contacts, 4 rows+warmstart, 5 Newton, 6 force+Euler solve, 7 (return) -> 8 obs prep,
 8 obs/reward write, 9 integrate+store.
@@ -71,7 +73,8 @@ def main():
     acts = torch.zeros(300, n, 2, device=dev)
     L.ackphys_random_actions(ctx, p(acts), 300, 0, 0, stream)
     summary = {}
-    for flags, label in [(2, "contacts OFF"), (3, "contacts ON")]:
+    # quad / obstacle kernels: contacts on only (the bench's contacts-off leg runs the lane kernel)
+    for flags, label in ([(3, "contacts ON")] if quad else [(2, "contacts OFF"), (3, "contacts ON")]):
         state.zero_()
         L.ackphys_reset(ctx, None, 0, p(state), p(obs), stream)
         for k in range(200):
@@ -121,7 +124,9 @@ def main():
         print(f"== {label}: median cycles per wave, total {tot:.0f}")
         for (_, _, name), v in zip(phases, d):
             print(f"  {name:16s} {v:10.0f}  {100 * v / tot:5.1f}%")
-        kern = "obst_kernel" if obst else ("quad_kernel" if quad else ("nc_kernel" if flags == 2 else "kernel"))
+        kern = (("obst8_kernel" if ROLL > 1 else "obst_kernel") if obst else
+                ("quad_kernel" if quad else ("nc_kernel" if flags == 2 else "kernel")))
+        label = f"{label}, {'obstacle scene' if obst else 'flat scene'}, {'quad' if quad else 'lane'} mapping"
         summary[label] = {"kernel": ("ackphys_rollout_" if ROLL > 1 else "ackphys_step_") + kern,
                           "dyn_wave_cycles_per_step_median": float(tot),
                           "dyn_wave_cycles_per_step_max": float(np.max(np.concatenate(spans))),
@@ -129,10 +134,15 @@ def main():
                           "measured": "diag build (s_memtime stamps, ~+11 % cycles), 4096 envs, steps 200-209 after "
                                       "reset, " + (f"last step of {ROLL}-step rollout launches" if ROLL > 1
                                                    else "single-step launches")}
-    if os.environ.get("STAMPS_JSON"):
+    if os.environ.get("STAMPS_JSON"):  # merged into the file's other entries (one file for every kernel)
         import json
+        old = {}
+        if os.path.exists(os.environ["STAMPS_JSON"]):
+            with open(os.environ["STAMPS_JSON"]) as f:
+                old = json.load(f)
+        old.update(summary)
         with open(os.environ["STAMPS_JSON"], "w") as f:
-            json.dump(summary, f, indent=1)
+            json.dump(old, f, indent=1)
 
 
 if __name__ == "__main__":
