@@ -221,6 +221,12 @@ typedef struct {
    * them when the call starts), so the gradient launches copy it into LDS with plain DMA instead of
    * transposing the parameters. Same results bit for bit; ignored with the fused update (params2) */
   float* weight_image;
+  /* optional scratch (single-rank path; NULL: one shuffle and one statistics launch per epoch into
+   * perm / stats): [n_epochs][n_idx] int32 and [n_epochs][nmb][2] floats -- every epoch's shuffle
+   * and minibatch advantage statistics formed by ONE launch at the start of the call (the same
+   * values as the per-epoch launches) */
+  int32_t* perm_epochs;
+  float* stats_epochs;
 } ackppo_train_desc;
 
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch

@@ -84,7 +84,7 @@ class TrainDesc(C.Structure):
                 ("grad_norm_out", C.c_void_p), ("world", C.c_int), ("allreduce", C.c_void_p),
                 ("allreduce_user", C.c_void_p), ("params2", C.c_void_p), ("exp_avg2", C.c_void_p),
                 ("exp_avg_sq2", C.c_void_p), ("log_std_min", C.c_float),
-                ("weight_image", C.c_void_p)]
+                ("weight_image", C.c_void_p), ("perm_epochs", C.c_void_p), ("stats_epochs", C.c_void_p)]
 
 
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:

@@ -1542,12 +1542,9 @@ __device__ __forceinline__ uint32_t perm_hash(uint32_t x, uint32_t k) {
   x *= 0xC2B2AE35u;
   return x ^ (x >> 16);
 }
-extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int half, uint32_t k0, uint32_t k1,
-                                                                     uint32_t k2, uint32_t k3, int32_t* out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t mask = (1u << half) - 1u, keys[4] = {k0, k1, k2, k3};
-  uint32_t x = (uint32_t)i;
+__device__ __forceinline__ uint32_t perm_at(uint32_t i, int n, int half, const uint32_t keys[4]) {
+  const uint32_t mask = (1u << half) - 1u;
+  uint32_t x = i;
   do {
     uint32_t L = x >> half, R = x & mask;
 #pragma unroll
@@ -1558,7 +1555,88 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int 
     }
     x = (L << half) | R;
   } while (x >= (uint32_t)n);
-  out[i] = (int32_t)x;
+  return x;
+}
+// the round keys of (seed, epoch): splitmix64 of seed ^ golden * (epoch + 1)
+__host__ __device__ inline void perm_keys(uint64_t seed, uint32_t epoch, uint32_t k[4]) {
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * ((uint64_t)epoch + 1));
+  for (int r = 0; r < 4; r++) {
+    z += 0x9E3779B97F4A7C15ull;
+    uint64_t y = z;
+    y = (y ^ (y >> 30)) * 0xBF58476D1CE4E5B9ull;
+    y = (y ^ (y >> 27)) * 0x94D049BB133111EBull;
+    k[r] = (uint32_t)(y ^ (y >> 31));
+  }
+}
+__host__ __device__ inline int perm_half(int n) {
+  int bits = 1;
+  while ((1u << bits) < (uint32_t)n) bits++;
+  return (bits + 1) / 2;
+}
+extern "C" __global__ void __launch_bounds__(256) ackppo_perm_kernel(int n, int half, uint32_t k0, uint32_t k1,
+                                                                     uint32_t k2, uint32_t k3, int32_t* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t keys[4] = {k0, k1, k2, k3};
+  out[i] = (int32_t)perm_at((uint32_t)i, n, half, keys);
+}
+
+// Every epoch's shuffle and minibatch advantage statistics of one ackppo_train call in ONE launch
+// (the advantages do not change during the call): workgroup (m, e) computes positions
+// [m B, (m + 1) B) of epoch e's permutation (the Feistel map above, keys of epoch epoch0 + e),
+// writes them to perm[e][.], gathers the advantages and forms minibatch m's statistics with
+// ackppo_adv_stats_kernel's arithmetic (the same bits). Replaces 2 launches per epoch.
+extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_perm_stats_kernel(const float* adv, int n, int batch,
+                                                                                   uint64_t seed, uint32_t epoch0,
+                                                                                   int normalize, int32_t* perm,
+                                                                                   float* stats) {
+  __shared__ double red[ADV_THREADS / 64];
+  const int m = blockIdx.x, e = blockIdx.y, tid = threadIdx.x, nmb = gridDim.x;
+  uint32_t keys[4];
+  perm_keys(seed, epoch0 + (uint32_t)e, keys);
+  const int half = perm_half(n);
+  int32_t* out = perm + (size_t)e * n;
+  float* st = stats + 2 * ((size_t)e * nmb + m);
+  const int lo = m * batch, hi = min(lo + batch, n), cnt = hi - lo;
+  float v[ADV_CACHE];
+  double s = 0.0;
+#pragma unroll
+  for (int c = 0; c < ADV_CACHE; c++) {
+    const int i = lo + tid + c * ADV_THREADS;
+    v[c] = 0.0f;
+    if (i < hi) {
+      const uint32_t x = perm_at((uint32_t)i, n, half, keys);
+      out[i] = (int32_t)x;
+      v[c] = adv[x];
+    }
+    s += v[c];
+  }
+  for (int i = lo + tid + ADV_CACHE * ADV_THREADS; i < hi; i += ADV_THREADS) {
+    const uint32_t x = perm_at((uint32_t)i, n, half, keys);
+    out[i] = (int32_t)x;
+    s += adv[x];
+  }
+  if (!normalize || cnt <= 1) {
+    if (tid == 0) { st[0] = 0.0f; st[1] = 1.0f; }
+    return;
+  }
+  const double mean = block_sum_d(s, red) / cnt;
+  double q = 0.0;
+#pragma unroll
+  for (int c = 0; c < ADV_CACHE; c++) {
+    const double d = (double)v[c] - mean;
+    q += (lo + tid + c * ADV_THREADS < hi) ? d * d : 0.0;
+  }
+  for (int i = lo + tid + ADV_CACHE * ADV_THREADS; i < hi; i += ADV_THREADS) {
+    const double d = adv[out[i]] - mean;  // this thread's own write above
+    q += d * d;
+  }
+  const double var = block_sum_d(q, red) / (cnt - 1);
+  if (tid == 0) {
+    const float sd = (float)sqrt(var);
+    st[0] = (float)mean;
+    st[1] = 1.0f / (sd + 1e-8f);
+  }
 }
 
 // Two passes, no atomics, no scratch: (1) grid (param blocks of 256, RG row groups) sums rows
@@ -1892,19 +1970,9 @@ int ackppo_gae(const float* rewards, const float* values, const float* episode_s
 int ackppo_permutation(int n, uint64_t seed, uint32_t epoch, int32_t* out, void* stream) {
   if (!out || n < 0 || n > (1 << 30)) return fail(ACKPPO_EINVAL, "ackppo_permutation: bad arguments");
   if (n == 0) return ACKPPO_OK;
-  int bits = 1;
-  while ((1u << bits) < (uint32_t)n) bits++;
-  const int half = (bits + 1) / 2;
-  // round keys: splitmix64 of (seed, epoch)
-  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * ((uint64_t)epoch + 1));
+  const int half = perm_half(n);
   uint32_t k[4];
-  for (int r = 0; r < 4; r++) {
-    z += 0x9E3779B97F4A7C15ull;
-    uint64_t y = z;
-    y = (y ^ (y >> 30)) * 0xBF58476D1CE4E5B9ull;
-    y = (y ^ (y >> 27)) * 0x94D049BB133111EBull;
-    k[r] = (uint32_t)(y ^ (y >> 31));
-  }
+  perm_keys(seed, epoch, k);  // round keys: splitmix64 of (seed, epoch)
   hipLaunchKernelGGL(ackppo_perm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, half, k[0], k[1],
                      k[2], k[3], out);
   return launched("ackppo_permutation");
@@ -2076,11 +2144,22 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     step_size = (float)(d->learning_rate / (1.0 - pow(d->beta1, tt)));
     bc2 = (float)sqrt(1.0 - pow(d->beta2, tt));
   };
+  // single rank with the per-call buffers: every epoch's shuffle and statistics in one launch now
+  const bool all_epochs = !dp && d->perm_epochs && d->stats_epochs;
+  if (all_epochs) {
+    if (S > (1 << 30)) return fail(ACKPPO_EINVAL, "ackppo_train: n_idx too large for the shuffle");
+    hipLaunchKernelGGL(ackppo_perm_stats_kernel, dim3(nmb, d->n_epochs), dim3(ADV_THREADS), 0, st, d->advantages, S, B,
+                       d->perm_key, d->perm_epoch0, d->normalize_advantage, d->perm_epochs, d->stats_epochs);
+    if ((rc = launched("ackppo_train: shuffles and statistics"))) return rc;
+  }
   for (int ep = 0; ep < d->n_epochs; ep++) {
-    if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
-    if (!dp) {
+    const int32_t* perm = all_epochs ? d->perm_epochs + (size_t)ep * S : d->perm;
+    const float* stats = all_epochs ? d->stats_epochs + (size_t)ep * nmb * 2 : d->stats;
+    if (!all_epochs && !dp) {
+      if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
       if ((rc = ackppo_adv_stats(d->advantages, d->perm, S, B, d->normalize_advantage, d->stats, stream))) return rc;
-    } else {
+    } else if (dp) {
+      if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
       double* mom = d->moments;
       if ((rc = ackppo_adv_moments(d->advantages, d->perm, S, B, 0, mom, stream))) return rc;
       if ((rc = coll(mom, 2 * (int64_t)nmb, ACKPPO_F64, "advantage count/sum"))) return rc;
@@ -2090,8 +2169,8 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     }
     for (int m = 0; m < nmb; m++) {
       const int nb = S - m * B < B ? S - m * B : B;
-      GradArgs A{pv[cur], d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, d->perm + (size_t)m * B, nb,
-                 d->stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial};
+      GradArgs A{pv[cur], d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, perm + (size_t)m * B, nb,
+                 stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial};
       A.wimg = wimg;
       if (pending) {  // fused: the previous minibatch's Adam step, applied while this launch stages
         A.upd = d->grad;

@@ -179,6 +179,10 @@ class PPO:
         self.perm_key = (self.seed * 7919 + self.rank) & 0xFFFFFFFFFFFFFFFF
         self.perm_epoch = 0
         self.perm = torch.empty(self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
+        # every epoch's shuffle and statistics of one train() call, formed by one launch at its start
+        # (ackppo_train_desc perm_epochs / stats_epochs; the data-parallel path keeps per-epoch launches)
+        self.perm_epochs = torch.empty(self.n_epochs, self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
+        self.stats_epochs = torch.zeros(self.n_epochs, nmb, 2, **f32)
         # the all-reduce hook of the data-parallel update: RCCL (native communicator) on GPU nodes,
         # host-staged in gloo rehearsals; collective="rccl" at world 1 runs the data-parallel path over
         # a one-rank communicator (timing that path on one GPU)
@@ -295,6 +299,7 @@ class PPO:
         d.n_idx, d.batch = self.n_steps * self.n_envs, self.batch_size
         d.params, d.exp_avg, d.exp_avg_sq = (t.data_ptr() for t in (self.params, self.exp_avg, self.exp_avg_sq))
         d.perm, d.stats, d.moments = self.perm.data_ptr(), self.mb_stats.data_ptr(), self.mb_moments.data_ptr()
+        self.set_epoch_buffers(True, d)
         d.grad_partial, d.loss_partial = self.gpart.data_ptr(), self.lpart.data_ptr()
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
         d.world = self.world
@@ -302,6 +307,14 @@ class PPO:
         self.set_fuse_adam(False, d)
         self.set_weight_image(False, d)
         return d
+
+    def set_epoch_buffers(self, on: bool, d=None):
+        """on (default): every epoch's shuffle and advantage statistics of a train() call come from
+        one launch at its start (ackppo_train_desc perm_epochs / stats_epochs); off: one shuffle and
+        one statistics launch per epoch. The same values either way."""
+        d = self._desc if d is None else d
+        d.perm_epochs, d.stats_epochs = ((self.perm_epochs.data_ptr(), self.stats_epochs.data_ptr()) if on
+                                         else (None, None))
 
     def set_weight_image(self, on: bool, d=None):
         """on: the gradient launches copy each net's weights into LDS from a pre-laid-out image that

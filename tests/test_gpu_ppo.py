@@ -372,6 +372,31 @@ def test_train_matches_epoch_calls():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("normalize", [True, False])
+def test_train_options_bit_identical(normalize):
+    """ackppo_train's optional buffers change where work happens, not the result: every epoch's
+    shuffle and statistics from one launch (perm_epochs / stats_epochs; here with a 10 000-sample
+    minibatch, past the statistics kernel's 8 192 register-cached samples, and a ragged last one) or
+    per-epoch launches, and the gradient kernel staging from the weight image or from the
+    parameters -- the same parameters, Adam moments and losses, bit for bit."""
+    from mujoco_playground_amd.rl import make_ackermann_env
+    from mujoco_playground_amd.rl.ppo import PPO
+    out = []
+    for epochs_buf, image in ((True, False), (False, False), (True, True), (False, True)):
+        venv = make_ackermann_env(env_type="vec", num_envs=1024, max_episode_steps=64, device=DEV)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=10000, n_epochs=2, seed=11, ent_coef=0.01,
+                    normalize_advantage=normalize)
+        model.set_epoch_buffers(epochs_buf)
+        model.set_weight_image(image)
+        model.learn(total_timesteps=2 * 16 * 1024)
+        out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.logger["train/value_loss"],
+                    model.logger["train/approx_kl"]))
+    for o in out[1:]:
+        np.testing.assert_array_equal(out[0][0], o[0])
+        np.testing.assert_array_equal(out[0][1], o[1])
+        assert out[0][2:] == o[2:]
+
+
 @pytest.mark.parametrize("variant", [{}, {"action_repeat": 5, "nohit_clear": True}])
 def test_obstacle_scene_ppo_4096(variant):
     """PPO on the obstacle scene at the bench's per-GPU shape (4096 envs; the fused rollout in the obst8

@@ -40,8 +40,10 @@ def main(scene):
         torch.cuda.synchronize()
         s = stamps.cpu().numpy()[: NSTAMP * nb].reshape(NSTAMP, nb).astype(np.int64)
         ok = (s[0] > 0) & (s[9] > 0) & (s[11] > 0) & (s[15] > 0) & (s[14] > 0)
+        ok &= (s[16] > 0) & (s[17] > 0) & (s[18] > 0) & (s[19] > 0)
         rows.append(np.stack([s[9] - s[0], s[12] - s[11], s[13] - s[12], s[14] - s[13], s[15] - s[14], s[15] - s[9],
-                              s[11] - s[0], s[15] - s[11]])[:, ok])
+                              s[11] - s[0], s[15] - s[11], s[16] - s[13], s[17] - s[16], s[18] - s[17], s[19] - s[18],
+                              s[14] - s[19]])[:, ok])
     r = np.concatenate(rows, axis=1)
     names = ["dyn: loaded -> barrier 1", "obs: observation", "obs: bootstrap", "obs: policy",
              "obs: waits at barrier 1", "dyn: waits at barrier 1", "obs entry - dyn entry", "obs: entry -> past barrier 1"]
