@@ -148,12 +148,14 @@ int ackppo_adam(float* params, const float* grad, float* exp_avg, float* exp_avg
 
 /* One epoch of minibatch updates on a single rank (world 1: no all-reduce between the gradient
  * and the Adam step). For m in [0, ceil(n_idx / batch)): ackppo_grad on idx[m * batch ...] with
- * stats[2m .. 2m+1]; ackppo_reduce with the loss columns ADDED to loss_acc [8]; ackppo_adam with
- * grad_scale 1 and t = adam_step0 + m + 1 (step_size = learning_rate / (1 - beta1^t), bc2_sqrt =
- * sqrt(1 - beta2^t), float64 as torch computes them). The same kernels and arithmetic as the
- * per-minibatch calls (SB3 PPO.train, on_policy_algorithm / ppo.py:196-279 of SB3 2.7.0); the
- * loop runs on the host in C so the launches queue back to back. ackppo_train (below) runs
- * whole training phases, single-rank or data-parallel, the same way. */
+ * stats[2m .. 2m+1], the reduction of the partial rows (the loss columns ADDED to loss_acc [8])
+ * and the Adam step with grad_scale 1 and t = adam_step0 + m + 1 (step_size = learning_rate /
+ * (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t), float64 as torch computes them): ackppo_reduce +
+ * ackppo_adam's arithmetic, with the gradient sums over 8 row groups and the global norm in the
+ * blocked order of 128-parameter blocks (the reduction hands each block's sum of squares to the
+ * Adam launch; SB3 PPO.train, on_policy_algorithm / ppo.py:196-279 of SB3 2.7.0). The loop runs on
+ * the host in C so the launches queue back to back. ackppo_train (below) runs whole training
+ * phases, single-rank or data-parallel, with the same kernels. */
 int ackppo_epoch(float* params, const float* obs_rows, const float* actions, const float* old_log_prob,
                  const float* advantages, const float* returns, const int32_t* idx, int n_idx, int batch,
                  const float* stats, float clip_range, float ent_coef, float vf_coef, float max_grad_norm,
@@ -204,14 +206,6 @@ typedef struct {
   int world;
   ackppo_allreduce_fn allreduce;
   void* allreduce_user;
-  /* nullable [NPARAM] scratch, zero-filled once by the caller (never written outside the layout's
-   * parameters): with all three, each minibatch's Adam step is applied by the NEXT minibatch's
-   * gradient launch while it stages the weights (same arithmetic and bits as ackppo_adam, one
-   * launch less per minibatch), the parameter / moment vectors alternating between the caller's and
-   * these; the result ends in the caller's vectors */
-  float* params2;
-  float* exp_avg2;
-  float* exp_avg_sq2;
   /* opt-in entropy floor (not an SB3 parameter; -INFINITY = SB3, bit for bit): log_std is held at or
    * above this value after every Adam step, so the DiagGaussian's spread cannot collapse below
    * exp(log_std_min) */
@@ -219,7 +213,7 @@ typedef struct {
   /* optional scratch, 2 * ACKPPO_WIMAGE floats (NULL: off): each net's gradient-kernel weight block
    * in the kernel's LDS layout, written by every Adam step beside the parameters (and built from
    * them when the call starts), so the gradient launches copy it into LDS with plain DMA instead of
-   * transposing the parameters. Same results bit for bit; ignored with the fused update (params2) */
+   * transposing the parameters. Same results bit for bit */
   float* weight_image;
   /* optional scratch (single-rank path; NULL: one shuffle and one statistics launch per epoch into
    * perm / stats): [n_epochs][n_idx] int32 and [n_epochs][nmb][2] floats -- every epoch's shuffle
@@ -232,8 +226,10 @@ typedef struct {
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch
  * shuffle (ackppo_permutation), the advantage statistics of every minibatch (world 1:
  * ackppo_adv_stats; world > 1: ackppo_adv_moments phase 0 -> all-reduce of 2 x nmb f64 -> phase 1 ->
- * all-reduce of nmb f64 -> ackppo_adv_finalize), then per minibatch ackppo_grad -> reduce ->
- * [all-reduce of NPARAM f32] -> ackppo_adam (grad_scale 1/world). Every launch and collective is
+ * all-reduce of nmb f64 -> ackppo_adv_finalize), then per minibatch ackppo_grad -> the reduction ->
+ * the Adam step (world 1 without a hook; ackppo_epoch's launches), or the reduction -> all-reduce of
+ * NPARAM f32 -> the norm blocks' sums -> the Adam step (grad_scale 1/world; the same arithmetic).
+ * Every launch and collective is
  * enqueued back to back from this one call: no per-minibatch host round trip (the host never waits
  * on the device, unless the hook itself does). World 1 without a hook: the same launches as
  * ackppo_epoch per epoch, bit for bit. A hook at world 1 runs the data-parallel sequence over one

@@ -82,8 +82,7 @@ class TrainDesc(C.Structure):
                 ("stats", C.c_void_p), ("moments", C.c_void_p), ("grad_partial", C.c_void_p),
                 ("loss_partial", C.c_void_p), ("grad", C.c_void_p), ("loss_acc", C.c_void_p),
                 ("grad_norm_out", C.c_void_p), ("world", C.c_int), ("allreduce", C.c_void_p),
-                ("allreduce_user", C.c_void_p), ("params2", C.c_void_p), ("exp_avg2", C.c_void_p),
-                ("exp_avg_sq2", C.c_void_p), ("log_std_min", C.c_float),
+                ("allreduce_user", C.c_void_p), ("log_std_min", C.c_float),
                 ("weight_image", C.c_void_p), ("perm_epochs", C.c_void_p), ("stats_epochs", C.c_void_p)]
 
 

@@ -256,26 +256,13 @@ struct GradArgs {
   float clip, ent_coef, vf_coef;
   float* gpart;
   float* lpart;
-  // the previous minibatch's Adam step, applied while staging (ackppo_train; upd == nullptr: none):
-  // params (above) / m_in / v_in and the reduced gradient upd -> p_out / m_out / v_out (every
-  // workgroup computes its net's new values; the one with tile (index mod rows) == its row writes them)
-  const float* upd;
-  const float* m_in;
-  const float* v_in;
-  float* p_out;
-  float* m_out;
-  float* v_out;
-  float scale, max_norm, b1, b2, eps, step_size, bc2_sqrt;
-  float* norm_out;
-  float lsmin;  // opt-in log_std floor (ackppo_train_desc::log_std_min; -inf: none)
   const float* wimg;  // ackppo_grad1i: the weight image (ackppo_train_desc::weight_image)
 };
 
-// ---- Adam (torch.optim.Adam after clip_grad_norm_), shared by ackppo_adam_kernel and the update
-// fused into ackppo_grad1_kernel's staging so both give the same bits: the global norm of
-// scale * grad summed in one fixed order by every 256-thread workgroup (thread t: float4 j = t + 256 k
-// ascending, x^2 + y^2 + z^2 + w^2 each; wave shuffles; the four wave sums in order), then the
-// per-parameter update.
+// ---- Adam (torch.optim.Adam after clip_grad_norm_). Two global-norm orders: grad_norm256 (the
+// C-ABI ackppo_adam: every 256-thread workgroup sums scale * grad itself, thread t: float4
+// j = t + 256 k ascending, x^2 + y^2 + z^2 + w^2 each; wave shuffles; the four wave sums in order)
+// and the blocked order of the update kernels (norm_block_sq / norm_from_blocks below).
 struct AdamK {
   float scale, coef, b1, b2, eps, step_size, bc2_sqrt, lsmin;
 };
@@ -301,6 +288,36 @@ __device__ __forceinline__ float grad_norm256(const float* __restrict__ g, float
   ss = wave_sum(ss);
   __syncthreads();  // red may be in use
   if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  return sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+}
+// The blocked order (ackppo_reduce_adam_kernel, ackppo_adam_blocked_kernel; ackppo_train and
+// ackppo_epoch): norm block b (128 parameters, b < NB_N) contributes S_b = wave_sum of (scale g)^2
+// over parameters 128 b + lane plus the same over 128 b + 64 + lane; the norm is the square root of
+// a 256-lane tree over S_0 .. S_{NB_N - 1} (wave sums, then (w0 + w1) + (w2 + w3)). Each workgroup
+// forms its own S_b; a grid barrier makes all of them visible.
+constexpr int NB_P = 128, NB_N = (P + NB_P - 1) / NB_P;
+static_assert(NB_N <= 256, "one 256-lane tree over the norm blocks");
+// S_b of norm block b from threads 0-127 (thread t: parameter 128 b + t, gv its gradient; red: 2
+// floats of LDS); the value is returned to every thread
+__device__ __forceinline__ float norm_block_sq(float gv, float scale, int b, float* red) {
+  const int t = threadIdx.x;
+  const bool in = t < NB_P && NB_P * b + t < P;
+  const float x = in ? gv * scale : 0.0f;
+  const float s = wave_sum(x * x);
+  __syncthreads();  // red may be in use
+  if (t < NB_P && (t & 63) == 0) red[t >> 6] = s;
+  __syncthreads();
+  return red[0] + red[1];
+}
+// the norm from the blocks' S_b (sq[b * stride], b < NB_N: visible to this workgroup), on threads 0-255 (red: 4
+// floats of LDS); every thread of the workgroup gets it
+__device__ __forceinline__ float norm_from_blocks(const float* sq, int stride, float* red) {
+  const int t = threadIdx.x;
+  float v = t < NB_N ? sq[(size_t)t * stride] : 0.0f;
+  v = wave_sum(v);
+  __syncthreads();
+  if (t < 256 && (t & 63) == 0) red[t >> 6] = v;
   __syncthreads();
   return sqrtf((red[0] + red[1]) + (red[2] + red[3]));
 }
@@ -498,51 +515,6 @@ static_assert(TOTAL * 4 <= 160 * 1024, "grad2 workgroup LDS");
 __device__ __forceinline__ int sw(int row, int s) { return row * 16 + (s ^ (4 * ((row >> 2) & 3))); }
 }  // namespace g2
 
-// the staging of one net's weights; with an update (GradArgs::upd), each weight is first replaced by
-// its Adam step (adam_elem) -- the values the unfused ackppo_adam would have written -- and the
-// workgroup whose row is (element index mod rows) writes the new parameter and moments back
-template <bool UPD>
-__device__ __forceinline__ float stage_w4(const GradArgs& A, const AdamK& k, int off, int i4, int row, int nrow,
-                                          float4& out) {
-  const float4 pv = *reinterpret_cast<const float4*>(A.params + off + 4 * i4);
-  if constexpr (!UPD) {
-    out = pv;
-    return 0.0f;
-  } else {
-    const float4 gv = *reinterpret_cast<const float4*>(A.upd + off + 4 * i4);
-    const float4 mv = *reinterpret_cast<const float4*>(A.m_in + off + 4 * i4);
-    const float4 vv = *reinterpret_cast<const float4*>(A.v_in + off + 4 * i4);
-    float4 pn, mn, vn;
-    adam_elem(k, pv.x, gv.x, mv.x, vv.x, pn.x, mn.x, vn.x);
-    adam_elem(k, pv.y, gv.y, mv.y, vv.y, pn.y, mn.y, vn.y);
-    adam_elem(k, pv.z, gv.z, mv.z, vv.z, pn.z, mn.z, vn.z);
-    adam_elem(k, pv.w, gv.w, mv.w, vv.w, pn.w, mn.w, vn.w);
-    if (i4 % nrow == row) {
-      *reinterpret_cast<float4*>(A.p_out + off + 4 * i4) = pn;
-      *reinterpret_cast<float4*>(A.m_out + off + 4 * i4) = mn;
-      *reinterpret_cast<float4*>(A.v_out + off + 4 * i4) = vn;
-    }
-    out = pn;
-    return 0.0f;
-  }
-}
-template <bool UPD>
-__device__ __forceinline__ float stage_w1(const GradArgs& A, const AdamK& k, int idx, int row, int nrow) {
-  const float pv = A.params[idx];
-  if constexpr (!UPD) {
-    return pv;
-  } else {
-    float pn, mn, vn;
-    adam_elem(k, pv, A.upd[idx], A.m_in[idx], A.v_in[idx], pn, mn, vn);
-    if (idx == ACKPPO_OFF_LOG_STD || idx == ACKPPO_OFF_LOG_STD + 1) pn = ls_floor(k, pn);
-    if (idx % nrow == row) {
-      A.p_out[idx] = pn;
-      A.m_out[idx] = mn;
-      A.v_out[idx] = vn;
-    }
-    return pn;
-  }
-}
 // LDS weight layouts of the two grad kernels: ackppo_grad1 (g1: W1T swizzled, W2 swizzled) and
 // ackppo_grad2 (g2: padded row-major W1, W2 and W2^T)
 struct L1 {
@@ -558,8 +530,8 @@ struct L2 {
   }
   static constexpr int B1 = g2::B1, B2 = g2::B2, HW = g2::HW, HB = g2::HB;
 };
-template <bool UPD, class LY = L1, int NTHR = GRAD_THREADS>
-__device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, float* w, int net, int row, int nrow) {
+template <class LY = L1, int NTHR = GRAD_THREADS>
+__device__ __forceinline__ void stage_net(const float* __restrict__ params, float* w, int net) {
   // all global loads first (one latency), then the LDS writes: W1 (float4 rows of 79 inputs)
   // transposed and swizzled, W2 swizzled, the short vectors
   constexpr int N1 = H * NOBS / 4, IT1 = (N1 + NTHR - 1) / NTHR, IT2 = H * H / 4 / NTHR;
@@ -570,25 +542,23 @@ __device__ __forceinline__ void stage_net(const GradArgs& A, const AdamK& k, flo
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
     const int i = tid + j * NTHR;
-    if (i < N1) stage_w4<UPD>(A, k, o1, i, row, nrow, v[j]);
+    if (i < N1) v[j] = *reinterpret_cast<const float4*>(params + o1 + 4 * i);
   }
-  if constexpr (UPD) __builtin_amdgcn_sched_barrier(0);  // W1's four arrays, then W2's: bounded registers
 #pragma unroll
-  for (int j = 0; j < IT2; j++) stage_w4<UPD>(A, k, o2, tid + j * NTHR, row, nrow, v2[j]);
+  for (int j = 0; j < IT2; j++) v2[j] = *reinterpret_cast<const float4*>(params + o2 + 4 * (tid + j * NTHR));
   __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the scatter (one memory latency)
   // short vectors: threads 0-63 b1, b2 and the head rows; 64-67 the head biases / log_std
   float b1 = 0.f, b2 = 0.f, hw0 = 0.f, hw1 = 0.f, hs = 0.f;
   if (tid < H) {
-    b1 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + tid, row, nrow);
-    b2 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + tid, row, nrow);
-    hw0 = stage_w1<UPD>(A, k, (net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W) + tid, row, nrow);
-    if (!net) hw1 = stage_w1<UPD>(A, k, ACKPPO_OFF_ACT_W + H + tid, row, nrow);
+    b1 = params[(net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1) + tid];
+    b2 = params[(net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2) + tid];
+    hw0 = params[(net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W) + tid];
+    if (!net) hw1 = params[ACKPPO_OFF_ACT_W + H + tid];
   }
   const int sc = tid - H;  // actor: 0, 1 action_net.bias, 2, 3 log_std; critic: 0 value_net.bias
   const bool has_sc = sc >= 0 && sc < (net ? 1 : 4);
   if (has_sc)
-    hs = stage_w1<UPD>(A, k, net ? ACKPPO_OFF_VAL_B : (sc < 2 ? ACKPPO_OFF_ACT_B + sc : ACKPPO_OFF_LOG_STD + sc - 2),
-                       row, nrow);
+    hs = params[net ? ACKPPO_OFF_VAL_B : (sc < 2 ? ACKPPO_OFF_ACT_B + sc : ACKPPO_OFF_LOG_STD + sc - 2)];
 #pragma unroll
   for (int j = 0; j < IT1; j++) {
     const int i = tid + j * NTHR;
@@ -641,9 +611,7 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS) ackppo_wimage_kernel(
   float* w = img + net * g1::WIMG;
   for (int i = threadIdx.x; i < g1::WIMG; i += GRAD_THREADS) w[i] = 0.0f;
   __syncthreads();
-  GradArgs A{};
-  A.params = params;
-  stage_net<false, L1>(A, AdamK{}, w, net, 0, 1);
+  stage_net<L1>(params, w, net);
 }
 
 __device__ __forceinline__ float row_sum_t(const float* a) {  // 32 samples of one LDS tile row
@@ -693,7 +661,7 @@ __device__ __forceinline__ int vec_offset_g1(int net, int i) {
   return i < 192 ? ACKPPO_OFF_VAL_W + (i - 128) : ACKPPO_OFF_VAL_B;
 }
 
-template <bool UPD, bool IMG = false>
+template <bool IMG = false>
 __device__ __forceinline__ void grad1(const GradArgs& A) {
   using namespace g1;
   PRSTAMP(13);
@@ -747,14 +715,8 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
   // overlaps it; the registers they hold through the staging cost a few spill slots)
   if (AK_GRAD1_PREFETCH && grp0 < ngrp) loads(NT * grp0 + half);
-  AdamK ak{};
-  if constexpr (UPD) {  // the pending Adam step: the global norm first (every workgroup, same order)
-    const float norm = grad_norm256(A.upd, A.scale, tl + X);
-    ak = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
-    if (blockIdx.x == 0 && tid == 0 && A.norm_out) A.norm_out[0] = norm;
-  }
   if constexpr (IMG) stage_image<NTHR>(A.wimg + net * WIMG, w);
-  else stage_net<UPD, L1, NTHR>(A, ak, w, net, grp0, gstride);
+  else stage_net<L1, NTHR>(A.params, w, net);
 
   f4v gw1[5], gw2[4];
 #pragma unroll
@@ -1042,11 +1004,8 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
 extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1_kernel(GradArgs A) {
   grad1<false>(A);
 }
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1u_kernel(GradArgs A) {
-  grad1<true>(A);
-}
 extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) ackppo_grad1i_kernel(GradArgs A) {
-  grad1<false, true>(A);
+  grad1<true>(A);
 }
 
 // ---- ackppo_grad, one net per workgroup, 16 samples per WAVE (default, AK_PPO_GRAD2). Workgroup
@@ -1061,12 +1020,12 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) 
 // to 1; its weights are 0), the layer-2 bias gradient an extra gW2 column tile of ones, the head
 // weights' gradients an MFMA of the per-sample head gradients with H2.
 
-template <bool UPD>
 __device__ __forceinline__ void grad2(const GradArgs& A) {
   using namespace g2;
   PRSTAMP(13);
   PSTAMP(0);
-  extern __shared__ float tl[];
+  extern __shared__ float g2_lds[];  // (a plain function: its own name for the dynamic LDS)
+  float* tl = g2_lds;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int net = blockIdx.x & 1, tile0 = blockIdx.x >> 1, tstride = gridDim.x >> 1;
@@ -1105,13 +1064,7 @@ __device__ __forceinline__ void grad2(const GradArgs& A) {
     }
   };
   if (tile0 < ntiles) loads(tile0);
-  AdamK ak{};
-  if constexpr (UPD) {  // the pending Adam step: the global norm first (every workgroup, same order)
-    const float norm = grad_norm256(A.upd, A.scale, tl + SCR);
-    ak = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
-    if (blockIdx.x == 0 && tid == 0 && A.norm_out) A.norm_out[0] = norm;
-  }
-  stage_net<UPD, L2>(A, ak, w, net, tile0, tstride);
+  stage_net<L2>(A.params, w, net);
   __syncthreads();  // the weights are staged (the only barrier before the final reduction)
   PSTAMP(1);
 
@@ -1394,8 +1347,7 @@ __device__ __forceinline__ void grad2(const GradArgs& A) {
   PSTAMP(15);
   PRSTAMP(14);
 }
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2_kernel(GradArgs A) { grad2<false>(A); }
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2u_kernel(GradArgs A) { grad2<true>(A); }
+extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2_kernel(GradArgs A) { grad2(A); }
 
 // ---- ackppo_act: MFMA policy tile. 16 envs per 256-lane workgroup (4096 envs = 256 workgroups,
 // one per CU): the weights are staged as in ackppo_grad (transposed / swizzled), X [80][16],
@@ -1781,14 +1733,12 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const flo
   }
 }
 
-// clip_grad_norm_ + Adam over the whole vector: 256-thread workgroups, each forming the global norm
-// itself (grad_norm256: the order ackppo_grad1u_kernel's fused update uses, so the two give the same
-// bits) and updating 256 float4 of parameters in place
+// clip_grad_norm_ + Adam over the whole vector (the C-ABI ackppo_adam): 256-thread workgroups, each
+// forming the global norm itself (grad_norm256) and updating 256 float4 of parameters in place
 extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* params, const float* grad, float* m,
                                                                      float* v, float scale, float max_norm, float b1,
                                                                      float b2, float eps, float step_size,
-                                                                     float bc2_sqrt, float* norm_out, float lsmin,
-                                                                     float* wimg) {
+                                                                     float bc2_sqrt, float* norm_out, float lsmin) {
   __shared__ float red[4];
   // this thread's parameter and moments are loaded before the norm (their latency hides under it)
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -1813,13 +1763,121 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adam_kernel(float* para
   reinterpret_cast<float4*>(params)[j] = pn;
   reinterpret_cast<float4*>(m)[j] = mn;
   reinterpret_cast<float4*>(v)[j] = vn;
-  if (wimg) {  // the new parameters into the weight image as well (ackppo_grad1i stages from it)
-    const float o[4] = {pn.x, pn.y, pn.z, pn.w};
+}
+
+// ---- the update kernels of ackppo_train / ackppo_epoch: the reduction also forms each norm
+// block's S_b (norm_block_sq), so the Adam launch after it reads 147 words for the global norm
+// instead of re-reading the whole gradient. Workgroup b owns norm block b: parameters 128 b ..
+// 128 b + 127 (147 workgroups for 18 764 parameters); S_b goes to row 0, column 128 b of the
+// partial rows, which only workgroup b reads (and the next gradient launch rewrites).
+struct UpdArgs {
+  float* gpart;  // partial rows [nblk][P] (ackppo_grad); row 0 column 128 b: S_b after the reduction
+  int nblk;
+  const float* lpart;
+  float ent_coef;
+  float* grad;
+  float* loss;
+  int accumulate;
+  int sq;  // ackppo_reduce_norm_kernel: write S_b (0: the data-parallel path forms them after its all-reduce)
+  float* params;
+  float* m;
+  float* v;
+  float scale, max_norm, b1, b2, eps, step_size, bc2_sqrt, lsmin;
+  float* norm_out;
+  float* wimg;  // optional weight image kept in step (ackppo_train_desc::weight_image)
+};
+// the partial rows reduced (8 row groups x 128 parameters; rows g, g + 8, ... in blocks of four as
+// ackppo_reduce1_kernel) into grad, the loss rows on workgroup 0, and S_b
+constexpr int RA_G = 8;
+extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce_norm_kernel(UpdArgs A) {
+  __shared__ float red[RA_G][NB_P + 1];
+  __shared__ float lred[256];
+  __shared__ float nred[2];
+  const int tid = threadIdx.x, pl = tid & (NB_P - 1), g = tid / NB_P, b = blockIdx.x;
+  const int pidx = b * NB_P + pl;
+  const bool own = tid < NB_P && pidx < P;
+  constexpr int RK = GRAD_MAX_BLOCKS / RA_G;
+  static_assert(RK % 4 == 0, "row blocks of four");
+  float x[RK];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int ix = g1::wimg_index(4 * j + c);
-      if (ix >= 0) wimg[ix] = o[c];
+  for (int k = 0; k < RK; k++) {
+    const int r = g + k * RA_G;
+    x[k] = (pidx < P && r < A.nblk) ? A.gpart[(size_t)r * P + pidx] : 0.0f;
+  }
+  int nmain = 0;
+#pragma unroll
+  for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < RK / 4; j++)
+    if (j < nmain) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
     }
+#pragma unroll
+  for (int k = 0; k < RK; k++)
+    if (k >= 4 * nmain) acc[0] += x[k];
+  red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  float gv = 0.0f;
+  if (own) {
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < RA_G; k++) s += red[k][tid];
+    if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= A.ent_coef;
+    A.grad[pidx] = s;
+    gv = s;
+  }
+  if (b == 0) {  // loss rows: as ackppo_reduce1_kernel
+    const int slot = tid & 7, grp = tid >> 3;
+    float s = 0.0f;
+    if (tid < 256)
+      for (int r = grp; r < A.nblk; r += 32) s += A.lpart[(size_t)r * ACKPPO_NLOSS + slot];
+    if (tid < 256) lred[tid] = s;
+    __syncthreads();
+    for (int o = 128; o >= 8; o >>= 1) {
+      if (tid < o) lred[tid] += lred[tid + o];
+      __syncthreads();
+    }
+    if (tid < ACKPPO_NLOSS) A.loss[tid] = (A.accumulate ? A.loss[tid] : 0.0f) + lred[tid];
+  }
+  if (!A.sq) return;
+  const float sb = norm_block_sq(gv, A.scale, b, nred);  // every row read above is done (barriers)
+  if (tid == 0) A.gpart[(size_t)b * NB_P] = sb;
+}
+// S_b of the gradient as it is now (the data-parallel path: after its all-reduce)
+extern "C" __global__ void __launch_bounds__(NB_P) ackppo_norm_blocks_kernel(UpdArgs A) {
+  __shared__ float nred[2];
+  const int t = threadIdx.x, b = blockIdx.x, p = b * NB_P + t;
+  const float sb = norm_block_sq(p < P ? A.grad[p] : 0.0f, A.scale, b, nred);
+  if (t == 0) A.gpart[(size_t)b * NB_P] = sb;
+}
+// clip_grad_norm_ + Adam with the blocked norm: workgroup b updates norm block b's parameters
+extern "C" __global__ void __launch_bounds__(256) ackppo_adam_blocked_kernel(UpdArgs A) {
+  __shared__ float nred[4];
+  const int t = threadIdx.x, b = blockIdx.x, p = b * NB_P + t;
+  const bool own = t < NB_P && p < P;
+  float gv = 0.0f, pv = 0.0f, mv = 0.0f, vv = 0.0f;
+  if (own) {  // issued before the norm: their latency hides under it
+    gv = A.grad[p];
+    pv = A.params[p];
+    mv = A.m[p];
+    vv = A.v[p];
+  }
+  const float norm = norm_from_blocks(A.gpart, NB_P, nred);
+  const AdamK k = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
+  if (b == 0 && t == 0 && A.norm_out) A.norm_out[0] = norm;
+  if (!own) return;
+  float pn, mn, vn;
+  adam_elem(k, pv, gv, mv, vv, pn, mn, vn);
+  static_assert(ACKPPO_OFF_LOG_STD == 0, "log_std first");
+  if (p < 2) pn = ls_floor(k, pn);
+  A.params[p] = pn;
+  A.m[p] = mn;
+  A.v[p] = vn;
+  if (A.wimg) {  // the new parameter into the weight image as well (ackppo_grad1i stages from it)
+    const int ix = g1::wimg_index(p);
+    if (ix >= 0) A.wimg[ix] = pn;
   }
 }
 
@@ -1861,29 +1919,27 @@ bool policy_lds_ready() {
   g_policy_attr[dev] = true;
   return true;
 }
-bool g_grad1u_attr[MAX_DEV] = {};
 bool g_grad1i_attr[MAX_DEV] = {};
-// ackppo_grad's launch: two workgroups (actor, critic) per partial row; with A.upd, the variant that
-// applies the pending Adam step while staging (ackppo_train)
+// ackppo_grad's launch: two workgroups (actor, critic) per partial row; with A.wimg, the variant that
+// stages the weight image (ackppo_train)
 int grad_launch(const GradArgs& A, void* stream) {
   const int dev = current_device();
   if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
-  const bool upd = A.upd != nullptr, img = !upd && A.wimg != nullptr && !AK_PPO_GRAD2;
-  bool& ready = upd ? g_grad1u_attr[dev] : (img ? g_grad1i_attr[dev] : g_grad_attr[dev]);
+  const bool img = A.wimg != nullptr && !AK_PPO_GRAD2;
+  bool& ready = img ? g_grad1i_attr[dev] : g_grad_attr[dev];
   if (!ready) {
-    const void* kern = AK_PPO_GRAD2 ? (upd ? (const void*)ackppo_grad2u_kernel : (const void*)ackppo_grad2_kernel)
-                                    : (upd ? (const void*)ackppo_grad1u_kernel
-                                           : (img ? (const void*)ackppo_grad1i_kernel : (const void*)ackppo_grad1_kernel));
+    const void* kern = AK_PPO_GRAD2 ? (const void*)ackppo_grad2_kernel
+                                    : (img ? (const void*)ackppo_grad1i_kernel : (const void*)ackppo_grad1_kernel);
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS) != hipSuccess)
       return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
     ready = true;
   }
   const int nblk = ackppo_grad_blocks(A.batch);
   if (AK_PPO_GRAD2)
-    hipLaunchKernelGGL(upd ? ackppo_grad2u_kernel : ackppo_grad2_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
+    hipLaunchKernelGGL(ackppo_grad2_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
                        GRAD_LDS, (hipStream_t)stream, A);
   else
-    hipLaunchKernelGGL(upd ? ackppo_grad1u_kernel : (img ? ackppo_grad1i_kernel : ackppo_grad1_kernel), dim3(2 * nblk),
+    hipLaunchKernelGGL(img ? ackppo_grad1i_kernel : ackppo_grad1_kernel, dim3(2 * nblk),
                        dim3(GRAD_THREADS * g1::NT),
                        GRAD_LDS, (hipStream_t)stream, A);
   return launched("ackppo_grad");
@@ -2055,12 +2111,26 @@ int ackppo_reduce(float* grad_partial, const float* loss_partial, int nblk, floa
 namespace {
 int adam_launch(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, float grad_scale,
                 float max_grad_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
-                float* grad_norm_out, float lsmin, void* stream, float* wimg = nullptr) {
+                float* grad_norm_out, float lsmin, void* stream) {
   if (!params || !grad || !exp_avg || !exp_avg_sq) return fail(ACKPPO_EINVAL, "ackppo_adam: bad arguments");
   hipLaunchKernelGGL(ackppo_adam_kernel, dim3((P / 4 + 255) / 256), dim3(256), 0, (hipStream_t)stream, params, grad,
                      exp_avg, exp_avg_sq, grad_scale, max_grad_norm, beta1, beta2, eps, step_size, bc2_sqrt,
-                     grad_norm_out, lsmin, wimg);
+                     grad_norm_out, lsmin);
   return launched("ackppo_adam");
+}
+// torch's bias corrections of Adam step t, in float64 as the host path
+void adam_scalars(double lr, double beta1, double beta2, double t, float& step_size, float& bc2_sqrt) {
+  step_size = (float)(lr / (1.0 - pow(beta1, t)));
+  bc2_sqrt = (float)sqrt(1.0 - pow(beta2, t));
+}
+// one minibatch's reduction and Adam step (ackppo_epoch / ackppo_train, single rank): two launches,
+// the norm from the reduction's block sums
+int reduce_adam_launch(UpdArgs& U, void* stream) {
+  U.sq = 1;
+  hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(1024), 0, (hipStream_t)stream, U);
+  if (const int rc = launched("ackppo_reduce_norm")) return rc;
+  hipLaunchKernelGGL(ackppo_adam_blocked_kernel, dim3(NB_N), dim3(256), 0, (hipStream_t)stream, U);
+  return launched("ackppo_adam_blocked");
 }
 }  // namespace
 
@@ -2082,18 +2152,16 @@ int ackppo_epoch(float* params, const float* obs_rows, const float* actions, con
       adam_step0 < 0)
     return fail(ACKPPO_EINVAL, "ackppo_epoch: bad arguments");
   const int nmb = (n_idx + batch - 1) / batch;
+  UpdArgs U{grad_partial, 0, loss_partial, ent_coef, grad, loss_acc, 1, 1, params, exp_avg, exp_avg_sq,
+            1.0f, max_grad_norm, (float)beta1, (float)beta2, eps, 0.0f, 0.0f, -INFINITY, grad_norm_out, nullptr};
   for (int m = 0; m < nmb; m++) {
     const int nb = n_idx - m * batch < batch ? n_idx - m * batch : batch;
     int rc = ackppo_grad(params, obs_rows, actions, old_log_prob, advantages, returns, idx + (size_t)m * batch, nb,
                          stats + 2 * m, clip_range, ent_coef, vf_coef, grad_partial, loss_partial, stream);
     if (rc) return rc;
-    rc = reduce_launch(grad_partial, loss_partial, ackppo_grad_blocks(nb), ent_coef, grad, loss_acc, 1, stream);
-    if (rc) return rc;
-    const double t = (double)(adam_step0 + m + 1);  // torch's bias corrections, in float64 as the host path
-    rc = ackppo_adam(params, grad, exp_avg, exp_avg_sq, 1.0f, max_grad_norm, (float)beta1, (float)beta2, eps,
-                     (float)(learning_rate / (1.0 - pow(beta1, t))), (float)sqrt(1.0 - pow(beta2, t)), grad_norm_out,
-                     stream);
-    if (rc) return rc;
+    U.nblk = ackppo_grad_blocks(nb);
+    adam_scalars(learning_rate, beta1, beta2, (double)(adam_step0 + m + 1), U.step_size, U.bc2_sqrt);
+    if ((rc = reduce_adam_launch(U, stream))) return rc;
   }
   return ACKPPO_OK;
 }
@@ -2109,8 +2177,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
   const bool dp = d->allreduce != nullptr;
   if ((d->world > 1 && !dp) || (dp && !d->moments))
     return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
-  const bool fuse = d->params2 && d->exp_avg2 && d->exp_avg_sq2;
-  float* wimg = (fuse || AK_PPO_GRAD2) ? nullptr : d->weight_image;
+  float* wimg = AK_PPO_GRAD2 ? nullptr : d->weight_image;
   const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
@@ -2120,7 +2187,6 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     hipLaunchKernelGGL(ackppo_wimage_kernel, dim3(2), dim3(GRAD_THREADS), 0, st, d->params, wimg);
     if (const int rc0 = launched("ackppo_train: weight image")) return rc0;
   }
-  const float scale = 1.0f / (float)d->world;
   int rc;
   auto coll = [&](void* buf, int64_t count, int dtype, const char* what) -> int {
     g_err[0] = 0;
@@ -2133,17 +2199,6 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     }
     return ACKPPO_OK;
   };
-  // parameter / moment vectors: [0] the caller's, [1] the scratch (fused updates alternate)
-  float* pv[2] = {d->params, d->params2};
-  float* mv[2] = {d->exp_avg, d->exp_avg2};
-  float* vv[2] = {d->exp_avg_sq, d->exp_avg_sq2};
-  int cur = 0;
-  bool pending = false;  // an Adam step whose gradient is in d->grad, not yet applied
-  double t = 0.0;
-  auto adam_scalars = [&](double tt, float& step_size, float& bc2) {  // torch's bias corrections, float64
-    step_size = (float)(d->learning_rate / (1.0 - pow(d->beta1, tt)));
-    bc2 = (float)sqrt(1.0 - pow(d->beta2, tt));
-  };
   // single rank with the per-call buffers: every epoch's shuffle and statistics in one launch now
   const bool all_epochs = !dp && d->perm_epochs && d->stats_epochs;
   if (all_epochs) {
@@ -2152,6 +2207,9 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
                        d->perm_key, d->perm_epoch0, d->normalize_advantage, d->perm_epochs, d->stats_epochs);
     if ((rc = launched("ackppo_train: shuffles and statistics"))) return rc;
   }
+  UpdArgs U{d->grad_partial, 0, d->loss_partial, d->ent_coef, d->grad, d->loss_acc, 1, 1, d->params, d->exp_avg,
+            d->exp_avg_sq, 1.0f / (float)d->world, d->max_grad_norm, (float)d->beta1, (float)d->beta2, d->eps, 0.0f,
+            0.0f, d->log_std_min, d->grad_norm_out, wimg};
   for (int ep = 0; ep < d->n_epochs; ep++) {
     const int32_t* perm = all_epochs ? d->perm_epochs + (size_t)ep * S : d->perm;
     const float* stats = all_epochs ? d->stats_epochs + (size_t)ep * nmb * 2 : d->stats;
@@ -2169,55 +2227,25 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     }
     for (int m = 0; m < nmb; m++) {
       const int nb = S - m * B < B ? S - m * B : B;
-      GradArgs A{pv[cur], d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, perm + (size_t)m * B, nb,
-                 stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial};
-      A.wimg = wimg;
-      if (pending) {  // fused: the previous minibatch's Adam step, applied while this launch stages
-        A.upd = d->grad;
-        A.m_in = mv[cur];
-        A.v_in = vv[cur];
-        A.p_out = pv[cur ^ 1];
-        A.m_out = mv[cur ^ 1];
-        A.v_out = vv[cur ^ 1];
-        A.scale = scale;
-        A.max_norm = d->max_grad_norm;
-        A.b1 = (float)d->beta1;
-        A.b2 = (float)d->beta2;
-        A.eps = d->eps;
-        adam_scalars(t, A.step_size, A.bc2_sqrt);
-        A.norm_out = d->grad_norm_out;
-        A.lsmin = d->log_std_min;
-        cur ^= 1;
-      }
+      GradArgs A{d->params, d->obs_rows, d->actions, d->old_log_prob, d->advantages, d->returns, perm + (size_t)m * B,
+                 nb, stats + 2 * m, d->clip_range, d->ent_coef, d->vf_coef, d->grad_partial, d->loss_partial, wimg};
       if ((rc = grad_launch(A, stream))) return rc;
-      if ((rc = reduce_launch(d->grad_partial, d->loss_partial, ackppo_grad_blocks(nb), d->ent_coef, d->grad,
-                              d->loss_acc, 1, stream)))
-        return rc;
-      if (dp && (rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
-      t = (double)(d->adam_step0 + (int64_t)ep * nmb + m + 1);
-      if (fuse) {
-        pending = true;
+      U.nblk = ackppo_grad_blocks(nb);
+      adam_scalars(d->learning_rate, d->beta1, d->beta2, (double)(d->adam_step0 + (int64_t)ep * nmb + m + 1),
+                   U.step_size, U.bc2_sqrt);
+      // single rank: the reduction (with the norm blocks' sums), the Adam step; data-parallel: the
+      // reduction, the gradient's all-reduce, the norm blocks' sums, the Adam step (the same order)
+      if (!dp) {
+        if ((rc = reduce_adam_launch(U, stream))) return rc;
       } else {
-        float ss, bc2;
-        adam_scalars(t, ss, bc2);
-        if ((rc = adam_launch(pv[cur], d->grad, mv[cur], vv[cur], scale, d->max_grad_norm, (float)d->beta1,
-                              (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream, wimg)))
-          return rc;
+        U.sq = 0;
+        hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(1024), 0, st, U);
+        if ((rc = launched("ackppo_train: reduction"))) return rc;
+        if ((rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
+        hipLaunchKernelGGL(ackppo_norm_blocks_kernel, dim3(NB_N), dim3(NB_P), 0, st, U);
+        hipLaunchKernelGGL(ackppo_adam_blocked_kernel, dim3(NB_N), dim3(256), 0, st, U);
+        if ((rc = launched("ackppo_train: Adam step"))) return rc;
       }
-    }
-  }
-  if (pending) {  // the last step, in place, then the result back into the caller's vectors
-    float ss, bc2;
-    adam_scalars(t, ss, bc2);
-    if ((rc = adam_launch(pv[cur], d->grad, mv[cur], vv[cur], scale, d->max_grad_norm, (float)d->beta1,
-                          (float)d->beta2, d->eps, ss, bc2, d->grad_norm_out, d->log_std_min, stream)))
-      return rc;
-    if (cur == 1) {
-      const size_t bytes = ACKPPO_NPARAM * sizeof(float);
-      if (hipMemcpyAsync(d->params, pv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-          hipMemcpyAsync(d->exp_avg, mv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-          hipMemcpyAsync(d->exp_avg_sq, vv[1], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return fail(ACKPPO_EHIP, "ackppo_train: copying the result back");
     }
   }
   return ACKPPO_OK;

@@ -165,8 +165,6 @@ class PPO:
         self.gpart = torch.zeros(nblk, NPARAM, **f32)  # pad words are never written: zero once
         self.lpart = torch.zeros(nblk, NLOSS, **f32)
         self.grad = torch.zeros(NPARAM, **f32)
-        # the alternate parameter / moment vectors of the fused Adam step (ackppo_train_desc params2 ...)
-        self.scratch = torch.zeros(3, NPARAM, **f32)
         # both nets' gradient-kernel weight blocks in the kernel's LDS layout (ackppo_train_desc weight_image)
         self.weight_image = torch.zeros(2 * _lib.ACKPPO_WIMAGE, **f32)
         self.loss = torch.zeros(NLOSS, **f32)
@@ -304,7 +302,6 @@ class PPO:
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
         d.world = self.world
         d.log_std_min = float("-inf") if self.log_std_min is None else float(self.log_std_min)
-        self.set_fuse_adam(False, d)
         self.set_weight_image(False, d)
         return d
 
@@ -325,16 +322,6 @@ class PPO:
         costs as much (4.99 -> 5.34)."""
         d = self._desc if d is None else d
         d.weight_image = self.weight_image.data_ptr() if on else None
-
-    def set_fuse_adam(self, on: bool, d=None):
-        """on: each minibatch's Adam step applied by the next gradient launch while it stages the
-        weights (one launch less per minibatch, the same bits); off (default): a separate ackppo_adam
-        launch each. Measured (profiles/r04f_ppo_timing.log): 41.9 us per minibatch fused against
-        38.7 us -- every one of the 512 gradient workgroups re-derives its net's Adam step (four
-        parameter-sized reads and the global norm), which costs more than the launch it saves."""
-        d = self._desc if d is None else d
-        ptrs = [t.data_ptr() for t in self.scratch] if on else [None, None, None]
-        d.params2, d.exp_avg2, d.exp_avg_sq2 = ptrs
 
     def set_collective(self, kind: str | None):
         """The update's all-reduce hook (shard.TrainerCollective): "rccl", "host", None = the

@@ -324,15 +324,14 @@ def test_train_paths_bit_identical():
     """PPO.train is one ackppo_train call. Its single-rank sequence (no hook), the data-parallel
     sequence over a one-rank native RCCL communicator (ackppo_rccl_allreduce: the world > 1 path with
     real RCCL calls) and over the host-staged hook (the gloo rehearsals' path, a no-op at world 1)
-    give bit-identical parameters, Adam moments and loss statistics -- with each Adam step fused into
-    the next gradient launch (default) or launched on its own."""
+    give bit-identical parameters, Adam moments and loss statistics: the single-rank reduction +
+    Adam launch and the data-parallel reduction -> all-reduce -> Adam launches share their order."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     out = []
-    for coll, fuse in ((None, True), ("rccl", True), ("host", True), (None, False), ("rccl", False)):
+    for coll in (None, "rccl", "host"):
         venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
         model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01, collective=coll)
-        model.set_fuse_adam(fuse)
         assert (model.collective is None) == (coll is None)
         model.learn(total_timesteps=2 * 16 * 256)
         out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
@@ -344,8 +343,8 @@ def test_train_paths_bit_identical():
 
 
 def test_train_matches_epoch_calls():
-    """ackppo_train (world 1, no hook, the Adam steps fused into the gradient launches) = per epoch
-    ackppo_permutation + ackppo_adv_stats + ackppo_epoch (grad -> reduce -> adam launches), bit for bit."""
+    """ackppo_train (world 1, no hook: every epoch's shuffle and statistics from one launch) = per epoch
+    ackppo_permutation + ackppo_adv_stats + ackppo_epoch (grad -> reduce + Adam launches), bit for bit."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
@@ -485,15 +484,16 @@ def test_ppo_learns_the_variant_task():
 
 def test_log_std_floor():
     """The opt-in entropy floor (log_std_min; include/ackppo.h): after every Adam step log_std >= the
-    floor -- a policy started below it is lifted to it at the first update -- the same bits with the
-    Adam step fused into the gradient launch or on its own; None leaves the SB3 update untouched."""
+    floor -- a policy started below it is lifted to it at the first update -- the same bits on the
+    single-rank launch and on the data-parallel sequence (one-rank RCCL hook: separate Adam launch);
+    None leaves the SB3 update untouched."""
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
     out = []
-    for fuse in (True, False):
+    for coll in (None, "rccl"):
         venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
-        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=2, seed=3, log_std_min=-0.5)
-        model.set_fuse_adam(fuse)
+        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=2, seed=3, log_std_min=-0.5,
+                    collective=coll)
         model.params[:2] = -2.0
         model.learn(total_timesteps=2 * 16 * 256)
         ls = model.params[:2].cpu().numpy()

@@ -46,7 +46,9 @@ def main(scene):
                               s[14] - s[19]])[:, ok])
     r = np.concatenate(rows, axis=1)
     names = ["dyn: loaded -> barrier 1", "obs: observation", "obs: bootstrap", "obs: policy",
-             "obs: waits at barrier 1", "dyn: waits at barrier 1", "obs entry - dyn entry", "obs: entry -> past barrier 1"]
+             "obs: waits at barrier 1", "dyn: waits at barrier 1", "obs entry - dyn entry", "obs: entry -> past barrier 1",
+             "policy: layer 1 (+ head rows)", "policy: layer 2", "policy: heads", "policy: rollout rows",
+             "policy: sample + controller"]
     print(f"== {scene} scene, PPO rollout step T-2, {r.shape[1]} workgroup samples; cycles (median / p90)")
     for nm, v in zip(names, r):
         print(f"  {nm:30s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")

@@ -1,11 +1,10 @@
-"""Where a PPO update's time goes: one rollout (4096 envs x 32 steps), then PPO.train() timed with the
-Adam step fused into the gradient launch or on its own, with and without the weight image
-(event-timed, 3 calls each). Under
+"""Where a PPO update's time goes: one rollout (4096 envs x 32 steps), then PPO.train() timed with
+and without the all-epochs shuffle buffers and the weight image (event-timed, 3 calls each). Under
 `rocprofv3 --kernel-trace` (tools/gpu_r04f.sh) the kernel trace then gives each kernel's duration
 and the idle gaps between consecutive kernels (tools/probes/ppo_update_timeline.py --trace DIR).
 
     python tools/probes/ppo_update_timeline.py              (timing)
-    python tools/probes/ppo_update_timeline.py --only 0,1    (one configuration: fuse_adam, weight_image)
+    python tools/probes/ppo_update_timeline.py --only 1,0    (one configuration: epoch_buffers, weight_image)
     python tools/probes/ppo_update_timeline.py --trace DIR  (summarise a rocprofv3 kernel trace)
 """
 import csv
@@ -17,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 
-def timing(configs=((False, True), (False, False), (True, False), (False, True), (False, False), (True, False))):
+def timing(configs=((True, False), (True, True), (False, False), (True, False), (True, True), (False, False))):
     import torch
     from mujoco_playground_amd.rl import AckermannVecEnv
     from mujoco_playground_amd.rl.ppo import PPO
@@ -26,8 +25,8 @@ def timing(configs=((False, True), (False, False), (True, False), (False, True),
     model = PPO("MlpPolicy", venv, n_steps=32, batch_size=8192, n_epochs=10, seed=0)
     model.collect_rollouts()
     nmb = 32 * 4096 // 8192 * 10
-    for fuse, img in configs:
-        model.set_fuse_adam(fuse)
+    for epochs, img in configs:
+        model.set_epoch_buffers(epochs)
         model.set_weight_image(img)
         model.train()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -38,7 +37,7 @@ def timing(configs=((False, True), (False, False), (True, False), (False, True),
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 3
-        print(f"fuse_adam={fuse} weight_image={img}: train() {ms:.3f} ms = {ms * 1e3 / nmb:.2f} us per minibatch",
+        print(f"epoch_buffers={epochs} weight_image={img}: train() {ms:.3f} ms = {ms * 1e3 / nmb:.2f} us per minibatch",
               flush=True)
 
 
@@ -67,7 +66,7 @@ def trace(d):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--trace":
         trace(sys.argv[2])
-    elif len(sys.argv) > 2 and sys.argv[1] == "--only":  # one configuration (for a kernel trace): FUSE,IMAGE
+    elif len(sys.argv) > 2 and sys.argv[1] == "--only":  # one configuration (for a kernel trace): EPOCH_BUFFERS,IMAGE
         f, i = (bool(int(v)) for v in sys.argv[2].split(","))
         timing(((f, i),))
     else:
