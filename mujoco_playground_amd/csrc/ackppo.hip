@@ -291,11 +291,11 @@ __device__ __forceinline__ float grad_norm256(const float* __restrict__ g, float
   __syncthreads();
   return sqrtf((red[0] + red[1]) + (red[2] + red[3]));
 }
-// The blocked order (ackppo_reduce_adam_kernel, ackppo_adam_blocked_kernel; ackppo_train and
+// The blocked order (ackppo_reduce_norm_kernel, ackppo_adam_blocked_kernel; ackppo_train and
 // ackppo_epoch): norm block b (128 parameters, b < NB_N) contributes S_b = wave_sum of (scale g)^2
 // over parameters 128 b + lane plus the same over 128 b + 64 + lane; the norm is the square root of
 // a 256-lane tree over S_0 .. S_{NB_N - 1} (wave sums, then (w0 + w1) + (w2 + w3)). Each workgroup
-// forms its own S_b; a grid barrier makes all of them visible.
+// forms its own S_b in the reduction; the Adam launch after it reads all of them.
 constexpr int NB_P = 128, NB_N = (P + NB_P - 1) / NB_P;
 static_assert(NB_N <= 256, "one 256-lane tree over the norm blocks");
 // S_b of norm block b from threads 0-127 (thread t: parameter 128 b + t, gv its gradient; red: 2
@@ -1786,13 +1786,31 @@ struct UpdArgs {
   float* norm_out;
   float* wimg;  // optional weight image kept in step (ackppo_train_desc::weight_image)
 };
+// Adam on norm block b's parameters once every S_b is visible: threads 0-127 own parameter 128 b + t
+// (gv its gradient, pv / mv / vv loaded earlier), threads 0-255 form the norm
+__device__ __forceinline__ void adam_block_update(const UpdArgs& A, int b, float gv, float pv, float mv, float vv,
+                                                  float* nred) {
+  const int t = threadIdx.x, p = b * NB_P + t;
+  const float norm = norm_from_blocks(A.gpart, NB_P, nred);
+  const AdamK k = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
+  if (b == 0 && t == 0 && A.norm_out) A.norm_out[0] = norm;
+  if (t >= NB_P || p >= P) return;
+  float pn, mn, vn;
+  adam_elem(k, pv, gv, mv, vv, pn, mn, vn);
+  static_assert(ACKPPO_OFF_LOG_STD == 0, "log_std first");
+  if (p < 2) pn = ls_floor(k, pn);
+  A.params[p] = pn;
+  A.m[p] = mn;
+  A.v[p] = vn;
+  if (A.wimg) {  // the new parameter into the weight image as well (ackppo_grad1i stages from it)
+    const int ix = g1::wimg_index(p);
+    if (ix >= 0) A.wimg[ix] = pn;
+  }
+}
 // the partial rows reduced (8 row groups x 128 parameters; rows g, g + 8, ... in blocks of four as
 // ackppo_reduce1_kernel) into grad, the loss rows on workgroup 0, and S_b
 constexpr int RA_G = 8;
-extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce_norm_kernel(UpdArgs A) {
-  __shared__ float red[RA_G][NB_P + 1];
-  __shared__ float lred[256];
-  __shared__ float nred[2];
+__device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P + 1], float* lred) {
   const int tid = threadIdx.x, pl = tid & (NB_P - 1), g = tid / NB_P, b = blockIdx.x;
   const int pidx = b * NB_P + pl;
   const bool own = tid < NB_P && pidx < P;
@@ -1841,6 +1859,14 @@ extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce_norm_kernel(Upd
     }
     if (tid < ACKPPO_NLOSS) A.loss[tid] = (A.accumulate ? A.loss[tid] : 0.0f) + lred[tid];
   }
+  return gv;
+}
+extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce_norm_kernel(UpdArgs A) {
+  __shared__ float red[RA_G][NB_P + 1];
+  __shared__ float lred[256];
+  __shared__ float nred[2];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const float gv = reduce_rows(A, red, lred);
   if (!A.sq) return;
   const float sb = norm_block_sq(gv, A.scale, b, nred);  // every row read above is done (barriers)
   if (tid == 0) A.gpart[(size_t)b * NB_P] = sb;
@@ -1864,21 +1890,7 @@ extern "C" __global__ void __launch_bounds__(256) ackppo_adam_blocked_kernel(Upd
     mv = A.m[p];
     vv = A.v[p];
   }
-  const float norm = norm_from_blocks(A.gpart, NB_P, nred);
-  const AdamK k = adam_k(norm, A.scale, A.max_norm, A.b1, A.b2, A.eps, A.step_size, A.bc2_sqrt, A.lsmin);
-  if (b == 0 && t == 0 && A.norm_out) A.norm_out[0] = norm;
-  if (!own) return;
-  float pn, mn, vn;
-  adam_elem(k, pv, gv, mv, vv, pn, mn, vn);
-  static_assert(ACKPPO_OFF_LOG_STD == 0, "log_std first");
-  if (p < 2) pn = ls_floor(k, pn);
-  A.params[p] = pn;
-  A.m[p] = mn;
-  A.v[p] = vn;
-  if (A.wimg) {  // the new parameter into the weight image as well (ackppo_grad1i stages from it)
-    const int ix = g1::wimg_index(p);
-    if (ix >= 0) A.wimg[ix] = pn;
-  }
+  adam_block_update(A, b, gv, pv, mv, vv, nred);
 }
 
 // ------------------------------------------------------------------ C-ABI

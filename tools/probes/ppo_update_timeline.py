@@ -66,8 +66,7 @@ def trace(d):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--trace":
         trace(sys.argv[2])
-    elif len(sys.argv) > 2 and sys.argv[1] == "--only":  # one configuration (for a kernel trace): EPOCH_BUFFERS,IMAGE
-        f, i = (bool(int(v)) for v in sys.argv[2].split(","))
-        timing(((f, i),))
+    elif len(sys.argv) > 2 and sys.argv[1] == "--only":  # one configuration (kernel traces): EPOCHS,IMAGE
+        timing((tuple(bool(int(v)) for v in sys.argv[2].split(",")),))
     else:
         timing()
