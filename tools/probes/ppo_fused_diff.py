@@ -1,7 +1,12 @@
 """GPU probe: where the fused PPO rollout and the per-step path differ (first mismatches per buffer).
-    python tools/probes/ppo_fused_diff.py [scene]"""
+    python tools/probes/ppo_fused_diff.py [scene [physics library under csrc/build]]"""
 import os
 import sys
+
+if len(sys.argv) > 2:  # another build of the physics library (before the first load)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from mujoco_playground_amd import _lib as _l
+    _l.LIB_PATH = os.path.join(os.path.dirname(_l.LIB_PATH), sys.argv[2])
 
 import torch
 
@@ -25,6 +30,9 @@ for name in BUFFERS:
             print("   ", i, float(x[tuple(i)]), float(y[tuple(i)]))
         if name == "buf_obs":
             rows = torch.nonzero(d.any(1)).flatten()
+            r0 = int(rows[0])
+            print("    row", r0, "fused  ", [round(float(v), 4) for v in x[r0, list(range(10)) + list(range(70, 79))]])
+            print("    row", r0, "perstep", [round(float(v), 4) for v in y[r0, list(range(10)) + list(range(70, 79))]])
             print("    steps", sorted(set((rows // n).tolist()))[:20], "cols", sorted(set(torch.nonzero(d)[:, 1].tolist())))
             st = (rows // n)
             env = rows % n
