@@ -1,9 +1,12 @@
 """GPU probe: host-clocked vs event-timed 20-step windows, the driver's bench shape
 (`--steps 20 --warmup 5`), under different preludes: a fresh sim right after start-up, after the
 ~0.2 s clock warm-up on a throwaway sim, and back to back. Prints one JSON line per window.
+With `spin` the HIP runtime is asked to spin-wait on synchronisation (hipDeviceScheduleSpin)
+before anything touches the GPU.
 
-    python tools/probes/short_window_probe.py
+    python tools/probes/short_window_probe.py [spin]
 """
+import ctypes
 import gc
 import json
 import os
@@ -50,6 +53,9 @@ FAST = False
 
 def main():
     global FAST
+    if len(sys.argv) > 1 and sys.argv[1] == "spin":
+        hip = ctypes.CDLL("libamdhip64.so")
+        print(json.dumps({"hipSetDeviceFlags(spin)": hip.hipSetDeviceFlags(ctypes.c_uint(1))}), flush=True)
     for FAST in (False, True):
         run()
 
