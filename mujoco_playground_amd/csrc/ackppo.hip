@@ -1810,32 +1810,74 @@ __device__ __forceinline__ void adam_block_update(const UpdArgs& A, int b, float
 // the partial rows reduced (8 row groups x 128 parameters; rows g, g + 8, ... in blocks of four as
 // ackppo_reduce1_kernel) into grad, the loss rows on workgroup 0, and S_b
 constexpr int RA_G = 8;
+// AK_PPO_RA_VEC: 16-B loads (a thread sums four adjacent parameters of its row group, 256 threads
+// per workgroup) -- per parameter the same rows in the same order as the scalar form (1024 threads)
+#ifndef AK_PPO_RA_VEC
+#define AK_PPO_RA_VEC 0
+#endif
+constexpr int RA_THREADS = AK_PPO_RA_VEC ? RA_G * NB_P / 4 : RA_G * NB_P;
 __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P + 1], float* lred) {
-  const int tid = threadIdx.x, pl = tid & (NB_P - 1), g = tid / NB_P, b = blockIdx.x;
-  const int pidx = b * NB_P + pl;
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int pidx = b * NB_P + tid;  // threads 0-127: the parameter this thread finishes
   const bool own = tid < NB_P && pidx < P;
   constexpr int RK = GRAD_MAX_BLOCKS / RA_G;
   static_assert(RK % 4 == 0, "row blocks of four");
-  float x[RK];
+  static_assert(P % 4 == 0 && NB_P % 4 == 0, "whole 16-B vectors per row and block");
+  if constexpr (AK_PPO_RA_VEC) {
+    const int pl4 = tid & (NB_P / 4 - 1), g = tid / (NB_P / 4);
+    const int vidx = b * (NB_P / 4) + pl4;
+    const bool vok = 4 * vidx < P;
+    float4 x[RK];
 #pragma unroll
-  for (int k = 0; k < RK; k++) {
-    const int r = g + k * RA_G;
-    x[k] = (pidx < P && r < A.nblk) ? A.gpart[(size_t)r * P + pidx] : 0.0f;
-  }
-  int nmain = 0;
-#pragma unroll
-  for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < RK / 4; j++)
-    if (j < nmain) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
+    for (int k = 0; k < RK; k++) {
+      const int r = g + k * RA_G;
+      // unconditional loads from valid addresses, zeros selected after (a conditional load compiles
+      // to an exec-masked branch that waits for it)
+      const float4 v = reinterpret_cast<const float4*>(A.gpart + (size_t)min(r, A.nblk - 1) * P)[min(vidx, P / 4 - 1)];
+      const bool ok = vok && r < A.nblk;
+      x[k] = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
     }
+    int nmain = 0;
 #pragma unroll
-  for (int k = 0; k < RK; k++)
-    if (k >= 4 * nmain) acc[0] += x[k];
-  red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < RK / 4; j++)
+        if (j < nmain) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[i] += R1Vec<4>::at(x[4 * j + i], c);
+        }
+#pragma unroll
+      for (int k = 0; k < RK; k++)
+        if (k >= 4 * nmain) acc[0] += R1Vec<4>::at(x[k], c);
+      red[g][4 * pl4 + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    }
+  } else {
+    const int pl = tid & (NB_P - 1), g = tid / NB_P;
+    const int pcol = b * NB_P + pl;
+    float x[RK];
+#pragma unroll
+    for (int k = 0; k < RK; k++) {
+      const int r = g + k * RA_G;
+      x[k] = (pcol < P && r < A.nblk) ? A.gpart[(size_t)r * P + pcol] : 0.0f;
+    }
+    int nmain = 0;
+#pragma unroll
+    for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < RK / 4; j++)
+      if (j < nmain) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
+      }
+#pragma unroll
+    for (int k = 0; k < RK; k++)
+      if (k >= 4 * nmain) acc[0] += x[k];
+    red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
   __syncthreads();
   float gv = 0.0f;
   if (own) {
@@ -1861,7 +1903,7 @@ __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P
   }
   return gv;
 }
-extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce_norm_kernel(UpdArgs A) {
+extern "C" __global__ void __launch_bounds__(RA_THREADS) ackppo_reduce_norm_kernel(UpdArgs A) {
   __shared__ float red[RA_G][NB_P + 1];
   __shared__ float lred[256];
   __shared__ float nred[2];
@@ -2139,7 +2181,7 @@ void adam_scalars(double lr, double beta1, double beta2, double t, float& step_s
 // the norm from the reduction's block sums
 int reduce_adam_launch(UpdArgs& U, void* stream) {
   U.sq = 1;
-  hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(1024), 0, (hipStream_t)stream, U);
+  hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(RA_THREADS), 0, (hipStream_t)stream, U);
   if (const int rc = launched("ackppo_reduce_norm")) return rc;
   hipLaunchKernelGGL(ackppo_adam_blocked_kernel, dim3(NB_N), dim3(256), 0, (hipStream_t)stream, U);
   return launched("ackppo_adam_blocked");
@@ -2251,7 +2293,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
         if ((rc = reduce_adam_launch(U, stream))) return rc;
       } else {
         U.sq = 0;
-        hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(1024), 0, st, U);
+        hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(RA_THREADS), 0, st, U);
         if ((rc = launched("ackppo_train: reduction"))) return rc;
         if ((rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
         hipLaunchKernelGGL(ackppo_norm_blocks_kernel, dim3(NB_N), dim3(NB_P), 0, st, U);
