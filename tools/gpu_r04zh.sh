@@ -21,3 +21,5 @@ print('$v$i', round(p['value']/1e6,2), round(p['update_us_per_minibatch'],2), ro
   done
 done
 cp $B/libackppo_ra0.so $B/libackppo.so
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ppo.py -q --timeout 240 --timeout-method thread > gpurun_out/r04zh_pytest_ra0.log 2>&1 || { echo TEST_RA0_FAIL; tail -30 gpurun_out/r04zh_pytest_ra0.log; exit 1; }
+tail -1 gpurun_out/r04zh_pytest_ra0.log
