@@ -155,27 +155,7 @@ def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_
     nmb = (n_steps * n_env + batch_size - 1) // batch_size
     dp_path = None
     if world == 1:
-        # the world > 1 update path on one GPU: ackppo_train's data-parallel sequence (advantage
-        # moments + 2 f64 all-reduces per epoch, one 75 KB f32 all-reduce per minibatch) over a one-rank
-        # native RCCL communicator, timed on the same rollout buffer (untimed first call)
-        model.set_collective("rccl")
-        model.train()
-        ed = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        torch.cuda.synchronize(device)
-        ed[0].record(stream)
-        for _ in range(iters):
-            model.train()
-        ed[1].record(stream)
-        torch.cuda.synchronize(device)
-        dp_ms = ed[0].elapsed_time(ed[1]) / iters
-        model.set_collective(None)
-        dp_path = {"update_ms": dp_ms, "update_us_per_minibatch": dp_ms * 1e3 / (nmb * n_epochs),
-                   "ratio_to_single_rank_update": dp_ms / train_ms,
-                   "collectives_per_iteration": n_epochs * (nmb + 2),
-                   "bytes_per_minibatch_allreduce": 4 * 18764,
-                   "note": "ackppo_train with the native RCCL hook (ackppo_rccl_allreduce) on a one-rank "
-                           "communicator: the data-parallel sequence every rank of configs[3] runs, each "
-                           "collective enqueued from C (no per-minibatch host round trip)"}
+        dp_path = time_dp_update(model, device, stream, iters, train_ms, n_epochs, nmb)
     return {"value": steps / el, "unit": "env-steps/s (rollout + update, all ranks)",
             "rollout_env_steps_per_s": n_steps * n_env * world / (roll_ms * 1e-3),
             "rollout_ms": roll_ms, "update_ms": train_ms, "minibatch_updates_per_iter": nmb * n_epochs,
@@ -185,6 +165,46 @@ def run_ppo(n_env, rank, world, device, iters=3, n_steps=32, batch_size=8192, n_
             "config": f"{scene} scene, {n_env} envs/GPU x {world}, n_steps {n_steps}, batch {batch_size} x {world} "
                       f"ranks, {n_epochs} epochs, contacts on, {iters} timed iterations after 1 warm-up",
             "last_logger": {k: v for k, v in model.logger.items() if isinstance(v, (int, float)) or v is None}}
+
+
+def time_dp_update(model, device, stream, iters, train_ms, n_epochs, nmb):
+    """The world > 1 update path timed on one GPU: ackppo_train's data-parallel sequence (every epoch's
+    shuffle and advantage moments at the start of the call with 2 f64 all-reduces, then per minibatch
+    the reduction, one 75 KB f32 all-reduce, the norm blocks and Adam) over a one-rank communicator,
+    on the same rollout buffer (untimed first call). "torch" = the default at world > 1: RCCL calls on
+    the communicator of torch's own ProcessGroupNCCL (a one-rank nccl process group here); "rccl" =
+    libackppo's own communicator (opt-in)."""
+    import torch.distributed as dist
+    out = {}
+    made_pg = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=device)
+        made_pg = True
+    try:
+        for kind in ("torch", "rccl"):
+            model.set_collective(kind)
+            model.train()
+            ed = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            torch.cuda.synchronize(device)
+            ed[0].record(stream)
+            for _ in range(iters):
+                model.train()
+            ed[1].record(stream)
+            torch.cuda.synchronize(device)
+            dp_ms = ed[0].elapsed_time(ed[1]) / iters
+            model.set_collective(None)
+            out[kind] = {"update_ms": dp_ms, "update_us_per_minibatch": dp_ms * 1e3 / (nmb * n_epochs),
+                         "ratio_to_single_rank_update": dp_ms / train_ms}
+    finally:
+        if made_pg:
+            dist.destroy_process_group()
+    d = dict(out["torch"])
+    d.update({"collective": "torch (the default at world > 1)", "native_communicator": out["rccl"],
+              "collectives_per_iteration": n_epochs * nmb + 2, "bytes_per_minibatch_allreduce": 4 * 18764,
+              "note": "ackppo_train with the RCCL hook on a one-rank communicator: the data-parallel sequence "
+                      "every rank of configs[3] runs, each collective enqueued from C (no per-minibatch host "
+                      "round trip); the advantage moments of all epochs in 2 collectives per train() call"})
+    return d
 
 
 def to_f64_state(st: torch.Tensor) -> np.ndarray:
@@ -349,11 +369,13 @@ def critical_path(kern_name: str, kern_ms: float):
         return None
     kc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
     ratio = e["dyn_wave_cycles_per_step_median"] / kc
+    frac = ratio / (1.0 + STAMP_OVERHEAD)
     return {"dyn_wave_cycles_per_step": e["dyn_wave_cycles_per_step_median"], "kernel_cycles_per_step": kc,
             "diag_over_kernel_cycles": ratio, "stamp_overhead": STAMP_OVERHEAD,
-            "frac_of_kernel_time": min(1.0, ratio / (1.0 + STAMP_OVERHEAD)), "clock_ghz_assumed": CLOCK_GHZ,
-            "note": "stamped diagnostic build (its stamps add ~11 %, removed in frac_of_kernel_time, which is "
-                    "clamped at 1) against this run's kernel time at the assumed peak clock",
+            "frac_of_kernel_time": frac, "consistent": frac <= 1.0, "clock_ghz_assumed": CLOCK_GHZ,
+            "note": "stamped diagnostic build (its stamps add ~11 %, removed in frac_of_kernel_time; not clamped: "
+                    "consistent = false when the stamped chain exceeds this run's kernel time, e.g. when the "
+                    "profile predates a kernel change) against this run's kernel time at the assumed peak clock",
             "phases_median": e.get("phases_median"),
             "source": f"profiles/critical_path_latest.json ({d.get('_round', '?')}): {e.get('measured', '')}"}
 

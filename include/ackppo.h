@@ -196,7 +196,7 @@ typedef struct {
   float* exp_avg_sq;
   int32_t* perm;            /* [n_idx] */
   float* stats;             /* [nmb][2] */
-  double* moments;          /* [3][nmb] (world > 1) */
+  double* moments;          /* with a hook: [3][nmb] float64, or [3][n_epochs][nmb] with perm_epochs / stats_epochs */
   float* grad_partial;      /* [ackppo_grad_blocks(batch)][NPARAM], pad words zero */
   float* loss_partial;      /* [ackppo_grad_blocks(batch)][8] */
   float* grad;              /* [NPARAM] */
@@ -215,10 +215,13 @@ typedef struct {
    * them when the call starts), so the gradient launches copy it into LDS with plain DMA instead of
    * transposing the parameters. Same results bit for bit */
   float* weight_image;
-  /* optional scratch (single-rank path; NULL: one shuffle and one statistics launch per epoch into
-   * perm / stats): [n_epochs][n_idx] int32 and [n_epochs][nmb][2] floats -- every epoch's shuffle
-   * and minibatch advantage statistics formed by ONE launch at the start of the call (the same
-   * values as the per-epoch launches) */
+  /* optional scratch (NULL: one shuffle and one statistics launch per epoch into perm / stats):
+   * [n_epochs][n_idx] int32 and [n_epochs][nmb][2] floats -- every epoch's shuffle and minibatch
+   * advantage statistics formed at the start of the call, the same values as the per-epoch launches
+   * (the advantages do not change during the call). Single rank: ONE launch. With a hook: one
+   * launch of every epoch's shuffle and (count, sum) into moments [0..1][n_epochs][nmb], ONE
+   * all-reduce of 2 x n_epochs x nmb f64, one launch of the squared deviations, ONE all-reduce of
+   * n_epochs x nmb f64, one finalize launch -- 2 collectives per call instead of 2 per epoch */
   int32_t* perm_epochs;
   float* stats_epochs;
 } ackppo_train_desc;
@@ -226,7 +229,8 @@ typedef struct {
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch
  * shuffle (ackppo_permutation), the advantage statistics of every minibatch (world 1:
  * ackppo_adv_stats; world > 1: ackppo_adv_moments phase 0 -> all-reduce of 2 x nmb f64 -> phase 1 ->
- * all-reduce of nmb f64 -> ackppo_adv_finalize), then per minibatch ackppo_grad -> the reduction ->
+ * all-reduce of nmb f64 -> ackppo_adv_finalize; with perm_epochs / stats_epochs all of it for every
+ * epoch at the start of the call), then per minibatch ackppo_grad -> the reduction ->
  * the Adam step (world 1 without a hook; ackppo_epoch's launches), or the reduction -> all-reduce of
  * NPARAM f32 -> the norm blocks' sums -> the Adam step (grad_scale 1/world; the same arithmetic).
  * Every launch and collective is
@@ -236,14 +240,18 @@ typedef struct {
  * rank (the same results: the moments give ackppo_adv_stats' statistics bit for bit). */
 int ackppo_train(const ackppo_train_desc* d, void* stream);
 
-/* Native RCCL communicator for the trainer's collectives (one process per GPU; the library is
- * the process's RCCL -- the one torch loaded if any, else librccl.so.1 -- opened at run time).
- * Rank 0 makes the 128-byte unique id, the caller distributes it (e.g. a torch.distributed
- * broadcast), every rank calls ackppo_rccl_init on its current device. */
+/* RCCL for the trainer's collectives (one process per GPU). The library is the RCCL already loaded
+ * in the process (torch's librccl.so.1; dlopen RTLD_NOLOAD -- never a second copy): these calls fail
+ * if none is loaded. ackppo_rccl_allreduce takes any communicator of that library: the one torch's
+ * ProcessGroupNCCL built (its _comm_ptr(); the default, shard.TrainerCollective kind "torch"), or one
+ * of this library's own (ackppo_rccl_unique_id on rank 0, the id distributed by the caller, then
+ * ackppo_rccl_init on every rank's current device; kind "rccl", opt-in).
+ * ackppo_rccl_library writes the path of the RCCL these calls use into `path` (0 = found). */
 int ackppo_rccl_unique_id(void* id128);
 int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm);
 int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void* stream); /* an ackppo_allreduce_fn */
 int ackppo_rccl_destroy(void* comm);
+int ackppo_rccl_library(char* path, int size);
 
 const char* ackppo_last_error(void);
 

@@ -129,7 +129,7 @@ PPO_EXPORTS = ["ackppo_act", "ackppo_act_boot", "ackppo_value", "ackppo_bootstra
                "ackppo_adv_moments", "ackppo_adv_finalize", "ackppo_grad",
                "ackppo_grad_blocks", "ackppo_reduce", "ackppo_adam", "ackppo_epoch", "ackppo_permutation",
                "ackppo_train", "ackppo_rccl_unique_id", "ackppo_rccl_init", "ackppo_rccl_allreduce",
-               "ackppo_rccl_destroy", "ackppo_last_error"]
+               "ackppo_rccl_destroy", "ackppo_rccl_library", "ackppo_last_error"]
 
 _lib = None
 _ppo = None
@@ -198,6 +198,7 @@ def ppo_lib():
     L.ackppo_rccl_init.argtypes = [P, i32, i32, C.POINTER(P)]
     L.ackppo_rccl_allreduce.argtypes = [P, i64, i32, P, P]
     L.ackppo_rccl_destroy.argtypes = [P]
+    L.ackppo_rccl_library.argtypes = [C.c_char_p, i32]
     L.ackppo_last_error.restype = C.c_char_p
     _ppo = L
     return L

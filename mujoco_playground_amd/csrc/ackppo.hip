@@ -196,12 +196,15 @@ extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_stats_kerne
 // all-reduces those rows, phase 1 writes the squared deviations about the GLOBAL mean into
 // moments[2][m]; after the second all-reduce, ackppo_adv_finalize forms the stats. The sums are
 // the single-rank kernel's, so world 1 reproduces ackppo_adv_stats bit for bit.
+// blockIdx.y = epoch e of an all-epoch launch (ackppo_train): idx rows [e][n_idx], moment rows
+// [3][E][nmb] (E = gridDim.y; E = 1 is the per-epoch layout [3][nmb]).
 extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_moments_kernel(const float* adv,
                                                                                     const int32_t* idx, int n_idx,
                                                                                     int batch, int phase, int nmb,
                                                                                     double* moments) {
   __shared__ double red[ADV_THREADS / 64];
-  const int m = blockIdx.x, tid = threadIdx.x;
+  const int m = blockIdx.x, tid = threadIdx.x, NM = nmb * gridDim.y, j = blockIdx.y * nmb + m;
+  idx += (size_t)blockIdx.y * n_idx;
   const int lo = m * batch, hi = min(lo + batch, n_idx), cnt = hi - lo;
   if (phase == 0) {
     double s = 0.0;
@@ -209,20 +212,20 @@ extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_adv_moments_ker
     // same per-lane order as ackppo_adv_stats_kernel: cached slots then the rest, all ascending
     const double tot = block_sum_d(s, red);
     if (tid == 0) {
-      moments[m] = (double)cnt;
-      moments[nmb + m] = tot;
-      moments[2 * nmb + m] = 0.0;
+      moments[j] = (double)cnt;
+      moments[NM + j] = tot;
+      moments[2 * NM + j] = 0.0;
     }
   } else {
-    const double n = moments[m];
-    const double mean = n > 0.0 ? moments[nmb + m] / n : 0.0;
+    const double n = moments[j];
+    const double mean = n > 0.0 ? moments[NM + j] / n : 0.0;
     double q = 0.0;
     for (int i = lo + tid; i < hi; i += ADV_THREADS) {
       const double d = (double)adv[idx[i]] - mean;
       q += d * d;
     }
     const double tot = block_sum_d(q, red);
-    if (tid == 0) moments[2 * nmb + m] = tot;
+    if (tid == 0) moments[2 * NM + j] = tot;
   }
 }
 extern "C" __global__ void __launch_bounds__(256) ackppo_adv_finalize_kernel(const double* moments, int nmb,
@@ -485,50 +488,12 @@ __device__ __forceinline__ int wimg_index(int p) {
   return base + B2 + (r - NW1 - H - NW2);
 }
 }  // namespace g1
-#ifndef AK_PPO_GRAD2
-#define AK_PPO_GRAD2 0
-#endif
-namespace g2 {
-constexpr int T = 64;                         // samples per workgroup tile
-// weights, row-major with padded rows (no swizzle: every MFMA operand address is a per-lane base
-// plus an immediate): W1 [64][84] (inputs 79.. zero), W2 [64][68] and its transpose W2T [64][68]
-// (A operands of layer 2 and of W2^T D2); the stride's residue (20, 4 mod 64) spreads a read of 16
-// rows x 4 columns over 64 banks
-constexpr int S1 = 84, S2 = 68;
-constexpr int W1 = 0, W2 = W1 + H * S1, W2T = W2 + H * S2, B1 = W2T + H * S2, B2 = B1 + H;
-constexpr int HW = B2 + H;                    // heads: actor [2][64] (critic [1][64])
-constexpr int HB = HW + 2 * H;                // actor: b[2], log_std[2] (critic: b[1])
-constexpr int WEND = HB + 4;
-constexpr int XS = 80 * 16, HS = 64 * 16;     // per wave: X [80][16], H [64][16] (H1 -> D1), G [64][16] (H2 -> D2)
-constexpr int VS = 4 * 16;                    // per wave: gmu [2][16], glog [2][16] (critic: gv [16])
-constexpr int WSCR = XS + 2 * HS + VS;
-constexpr int SCR = WEND;                     // per-wave scratch after the weights
-constexpr int TOTAL = SCR + 4 * WSCR;
-// the end-of-kernel reduction reuses the whole LDS: [4 waves][64][80] (gW1 and the b1 column), then
-// [4 waves][64][VROW] (gW2, b2, head weights)
-constexpr int VROW = 64 + 1 + 2;
-static_assert(4 * 64 * 80 <= TOTAL && 4 * 64 * VROW + 16 <= TOTAL, "reduction scratch");
-static_assert(TOTAL * 4 <= 160 * 1024, "grad2 workgroup LDS");
-// [row][sample] tile swizzle: the sample index XORed with 4 ((row >> 2) & 3), so both MFMA read
-// patterns -- B[k][sample] (4 rows x 16 samples) and B[sample][row] (16 rows x 4 samples) -- hit 64
-// distinct banks
-__device__ __forceinline__ int sw(int row, int s) { return row * 16 + (s ^ (4 * ((row >> 2) & 3))); }
-}  // namespace g2
 
-// LDS weight layouts of the two grad kernels: ackppo_grad1 (g1: W1T swizzled, W2 swizzled) and
-// ackppo_grad2 (g2: padded row-major W1, W2 and W2^T)
+// LDS weight layout of the grad kernel ackppo_grad1 (g1: W1T swizzled, W2 swizzled)
 struct L1 {
   static __device__ __forceinline__ void w1(float* w, int u, int k, float x) { w[g1::w1t(k, u)] = x; }
   static __device__ __forceinline__ void w2(float* w, int u, int k, float x) { w[g1::w2(u, k)] = x; }
   static constexpr int B1 = g1::B1, B2 = g1::B2, HW = g1::HW, HB = g1::HB;
-};
-struct L2 {
-  static __device__ __forceinline__ void w1(float* w, int u, int k, float x) { w[g2::W1 + u * g2::S1 + k] = x; }
-  static __device__ __forceinline__ void w2(float* w, int u, int k, float x) {
-    w[g2::W2 + u * g2::S2 + k] = x;
-    w[g2::W2T + k * g2::S2 + u] = x;
-  }
-  static constexpr int B1 = g2::B1, B2 = g2::B2, HW = g2::HW, HB = g2::HB;
 };
 template <class LY = L1, int NTHR = GRAD_THREADS>
 __device__ __forceinline__ void stage_net(const float* __restrict__ params, float* w, int net) {
@@ -1008,347 +973,6 @@ extern "C" __global__ void __launch_bounds__(GRAD_THREADS * g1::NT, 2 / g1::NT) 
   grad1<true>(A);
 }
 
-// ---- ackppo_grad, one net per workgroup, 16 samples per WAVE (default, AK_PPO_GRAD2). Workgroup
-// 2 t + net takes the actor (net 0) or the critic (net 1) of 64-sample tile t; wave w carries samples
-// 16 w .. 16 w + 15 of the tile through the whole forward / backward pass on its own -- every product
-// is [units x its 16 samples] (MFMA tiles of 16 units), its activations live in its own LDS scratch,
-// so no workgroup barrier separates the layers (ackppo_grad1's waves shared a 32-sample tile by unit
-// tiles: seven barriers per tile, one wave's stall held all four). The workgroup's four waves sum
-// their weight gradients once, at the end, through LDS (fixed order), and write one half-row (their
-// net) of the tile's partial gradient row: 128 rows per 8192-sample minibatch instead of 256.
-// Folded into the products: the layer-1 bias gradient is the gW1 column of the pad input row 79 (set
-// to 1; its weights are 0), the layer-2 bias gradient an extra gW2 column tile of ones, the head
-// weights' gradients an MFMA of the per-sample head gradients with H2.
-
-__device__ __forceinline__ void grad2(const GradArgs& A) {
-  using namespace g2;
-  PRSTAMP(13);
-  PSTAMP(0);
-  extern __shared__ float g2_lds[];  // (a plain function: its own name for the dynamic LDS)
-  float* tl = g2_lds;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int net = blockIdx.x & 1, tile0 = blockIdx.x >> 1, tstride = gridDim.x >> 1;
-  float* w = tl;
-  float* xs = tl + SCR + wave * WSCR;   // this wave's X, H, G, V scratch
-  float* hs1 = xs + XS;
-  float* gs2 = hs1 + HS;
-  float* vs = gs2 + HS;
-  const float invB = 1.0f / (float)A.batch;
-  const int ntiles = (A.batch + T - 1) / T;
-  const int li = lane & 15, lk = lane >> 4;
-  // the wave's 16 samples: lane (li, lk) gathers inputs k = lk, lk + 4, ... of sample li
-  float xg[20];
-  float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto loads = [&](int tile) __attribute__((always_inline)) {
-    const int s0 = tile * T + 16 * wave, nvalid = min(16, A.batch - s0);
-    const int sidx = A.idx[min(s0 + li, A.batch - 1)];  // a valid index for padding lanes too
-    const float* row = A.obs_rows + (size_t)sidx * NOBS;
-    const bool v = li < nvalid;
-#pragma unroll
-    for (int i = 0; i < 20; i++) {
-      const int k = lk + 4 * i;
-      const float x = row[min(k, NOBS - 1)];
-      xg[i] = k < NOBS ? (v ? x : 0.0f) : 1.0f;  // input row 79: the ones of the layer-1 bias gradient
-    }
-    if (net == 0) {
-      const float2 a = *reinterpret_cast<const float2*>(A.actions + 2 * (size_t)sidx);
-      const float o = A.old_logp[sidx], ad = A.adv[sidx];
-      hin[0] = v ? a.x : 0.0f;
-      hin[1] = v ? a.y : 0.0f;
-      hin[2] = v ? o : 0.0f;
-      hin[3] = v ? ad : 0.0f;
-    } else {
-      const float rt = A.ret[sidx];
-      hin[0] = v ? rt : 0.0f;
-    }
-  };
-  if (tile0 < ntiles) loads(tile0);
-  stage_net<L2>(A.params, w, net);
-  __syncthreads();  // the weights are staged (the only barrier before the final reduction)
-  PSTAMP(1);
-
-  // accumulators over the workgroup's tiles: gW1 [4 unit tiles][5 input tiles] (column 79 = b1),
-  // gW2 [4][4] (+ [4] ones column: b2), head weights [4 unit tiles] (rows 0-1 actor mu, row 0 critic)
-  f4v gw1[4][5], gw2[4][5], ghw[4];
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) gw1[t][j] = gw2[t][j] = f4v{0.f, 0.f, 0.f, 0.f};
-    ghw[t] = f4v{0.f, 0.f, 0.f, 0.f};
-  }
-  float la = 0.0f, lb = 0.0f, lc = 0.0f, ln = 0.0f;   // loss sums (lanes lk == 0: sample li)
-  float sab0 = 0.f, sab1 = 0.f, slg0 = 0.f, slg1 = 0.f;  // head bias / log_std gradient sums (actor; critic sab0)
-
-  for (int tile = tile0; tile < ntiles; tile += tstride) {
-    const int s0 = tile * T + 16 * wave, nvalid = min(16, A.batch - s0);
-    if (tile != tile0) loads(tile);
-#pragma unroll
-    for (int i = 0; i < 20; i++) xs[sw(lk + 4 * i, li)] = xg[i];
-    wave_lds_sync();
-    PSTAMP(2);
-    {  // layer 1: H1 [64 x 16] = tanh(W1 X + b1), four unit tiles
-      f4v a[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int k0 = 0; k0 < 80; k0 += 4) {
-        const int k = k0 + lk;
-        const float b = xs[sw(k, li)];
-#pragma unroll
-        for (int t = 0; t < 4; t++) a[t] = mfma4(w[W1 + (16 * t + li) * S1 + k], b, a[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = 16 * t + 4 * lk + r;
-          hs1[sw(u, li)] = ftanh(a[t][r] + w[B1 + u]);
-        }
-    }
-    wave_lds_sync();
-    PSTAMP(3);
-    {  // layer 2: H2 [64 x 16] = tanh(W2 H1 + b2)
-      f4v a[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;
-        const float b = hs1[sw(k, li)];
-#pragma unroll
-        for (int t = 0; t < 4; t++) a[t] = mfma4(w[W2 + (16 * t + li) * S2 + k], b, a[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = 16 * t + 4 * lk + r;
-          gs2[sw(u, li)] = ftanh(a[t][r] + w[B2 + u]);
-        }
-    }
-    wave_lds_sync();
-    PSTAMP(4);
-    // heads: lane (sample li, quarter lk) sums 16 of the 64 inputs (the quarter's rows rotated by lk:
-    // conflict-free), two butterflies over lk; every lane of sample li then holds its head outputs
-    const bool hvalid = li < nvalid;
-    float gm0 = 0.0f, gm1 = 0.0f;  // dL/dmu (actor) or dL/dV (critic, gm0) of sample li
-    if (net == 0) {
-      float m0 = 0.0f, m1 = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int k = 16 * lk + ((j + lk) & 15);
-        const float h = gs2[sw(k, li)];
-        m0 = fmaf(w[HW + k], h, m0);
-        m1 = fmaf(w[HW + H + k], h, m1);
-      }
-      m0 += __shfl_xor(m0, 16, 64);
-      m1 += __shfl_xor(m1, 16, 64);
-      m0 += __shfl_xor(m0, 32, 64);
-      m1 += __shfl_xor(m1, 32, 64);
-      const float mu0 = m0 + w[HB], mu1 = m1 + w[HB + 1];
-      const float ls0 = w[HB + 2], ls1 = w[HB + 3];
-      const float logp = gauss_term(hin[0], mu0, ls0) + gauss_term(hin[1], mu1, ls1);
-      const float lr = logp - hin[2];
-      const float r = fexp(lr);
-      const float adv = (hin[3] - A.stats[0]) * A.stats[1];
-      const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
-      const float l1 = adv * r, l2 = adv * rc;
-      // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
-      // gradient and the clamp passes it, so the sum is the full l1 gradient), else 0
-      const float glogp = hvalid ? ((l1 <= l2) ? -adv * r * invB : 0.0f) : 0.0f;
-      const float iv0 = fexp(-2.0f * ls0), iv1 = fexp(-2.0f * ls1);
-      const float dv0 = hin[0] - mu0, dv1 = hin[1] - mu1;
-      gm0 = glogp * dv0 * iv0;
-      gm1 = glogp * dv1 * iv1;
-      const float gl0 = glogp * (dv0 * dv0 * iv0 - 1.0f), gl1 = glogp * (dv1 * dv1 * iv1 - 1.0f);
-      if (lk == 0) {
-        vs[li] = gm0;
-        vs[16 + li] = gm1;
-        sab0 += gm0;
-        sab1 += gm1;
-        slg0 += gl0;
-        slg1 += gl1;
-        if (hvalid) {
-          la += -fminf(l1, l2);
-          lb += (fabsf(r - 1.0f) > A.clip) ? 1.0f : 0.0f;
-          lc += (r - 1.0f) - lr;
-          ln += 1.0f;
-        }
-      }
-    } else {
-      float v = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int k = 16 * lk + ((j + lk) & 15);
-        v = fmaf(w[HW + k], gs2[sw(k, li)], v);
-      }
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      v += w[HB];
-      const float R = hin[0];
-      gm0 = hvalid ? A.vf_coef * 2.0f * (v - R) * invB : 0.0f;
-      if (lk == 0) {
-        vs[li] = gm0;
-        sab0 += gm0;
-        if (hvalid) la += (R - v) * (R - v);
-      }
-    }
-    wave_lds_sync();
-    PSTAMP(5);
-    // head weights' gradient: [rows d x 64] += gmu [d x 16 samples] . H2^T (before D2 replaces H2)
-#pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 4) {
-      const int q = q0 + lk;
-      const float a = (li < (net ? 1 : 2)) ? vs[16 * li + q] : 0.0f;
-#pragma unroll
-      for (int t = 0; t < 4; t++) ghw[t] = mfma4(a, gs2[sw(16 * t + li, q)], ghw[t]);
-    }
-    // D2 = dL/dH2 (1 - H2^2) in place: lane (sample li, quarter lk) takes units 16 lk + ...
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const int u = 16 * lk + ((j + lk) & 15);
-      const float h = gs2[sw(u, li)];
-      const float dh = net ? gm0 * w[HW + u] : fmaf(gm0, w[HW + u], gm1 * w[HW + H + u]);
-      gs2[sw(u, li)] = dh * (1.0f - h * h);
-    }
-    wave_lds_sync();
-    PSTAMP(6);
-    {  // gW2 [64 x 64] += D2 H1^T and b2 (ones column tile); d1 = W2^T D2 (layer-1 units x 16)
-#pragma unroll
-      for (int q0 = 0; q0 < 16; q0 += 4) {
-        const int q = q0 + lk;  // sample
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const float a = gs2[sw(16 * t + li, q)];
-#pragma unroll
-          for (int j = 0; j < 4; j++) gw2[t][j] = mfma4(a, hs1[sw(16 * j + li, q)], gw2[t][j]);
-          gw2[t][4] = mfma4(a, 1.0f, gw2[t][4]);
-        }
-      }
-      f4v d[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;  // layer-2 unit
-        const float b = gs2[sw(k, li)];
-#pragma unroll
-        for (int t = 0; t < 4; t++) d[t] = mfma4(w[W2T + (16 * t + li) * S2 + k], b, d[t]);
-      }
-      wave_lds_sync();  // every read of H1 above is done: D1 replaces it
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int u = 16 * t + 4 * lk + r;
-          const float h = hs1[sw(u, li)];
-          hs1[sw(u, li)] = d[t][r] * (1.0f - h * h);
-        }
-    }
-    wave_lds_sync();
-    PSTAMP(7);
-    // gW1 [64 x 80] += D1 X^T (column 79: the ones row = b1)
-#pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 4) {
-      const int q = q0 + lk;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const float a = hs1[sw(16 * t + li, q)];
-#pragma unroll
-        for (int j = 0; j < 5; j++) gw1[t][j] = mfma4(a, xs[sw(16 * j + li, q)], gw1[t][j]);
-      }
-    }
-    wave_lds_sync();  // the next tile overwrites X
-    PSTAMP(8);
-  }
-  // ---- the workgroup's sums over its four waves (fixed order), written as its net's half-row
-  const int row = tile0;
-  float* g = A.gpart + (size_t)row * P;
-  const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ob1 = net ? ACKPPO_OFF_VF_B1 : ACKPPO_OFF_PI_B1;
-  const int ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2, ob2 = net ? ACKPPO_OFF_VF_B2 : ACKPPO_OFF_PI_B2;
-  const int ohw = net ? ACKPPO_OFF_VAL_W : ACKPPO_OFF_ACT_W;
-  __syncthreads();  // every wave's scratch is free
-  {  // gW1 + b1: [wave][unit][80]
-    float* r1 = tl + wave * 64 * 80;
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int j = 0; j < 5; j++) r1[(16 * t + 4 * lk + r) * 80 + 16 * j + li] = gw1[t][j][r];
-    __syncthreads();
-    // wave w sums units 16 w ..: 1280 values, 20 per lane
-    for (int i = lane; i < 16 * 80; i += 64) {
-      const int u = 16 * wave + i / 80, k = i % 80, o = u * 80 + k;
-      const float s = (tl[o] + tl[64 * 80 + o]) + (tl[2 * 64 * 80 + o] + tl[3 * 64 * 80 + o]);
-      if (k < NOBS) g[ow1 + u * NOBS + k] = s;
-      else g[ob1 + u] = s;
-    }
-    __syncthreads();
-  }
-  {  // gW2 + b2 + head weights: [wave][unit][VROW]
-    constexpr int VR = VROW;
-    float* r2 = tl + wave * 64 * VR;
-#pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int u = 16 * t + 4 * lk + r;
-#pragma unroll
-        for (int j = 0; j < 4; j++) r2[u * VR + 16 * j + li] = gw2[t][j][r];
-        if (li == 0) r2[u * VR + 64] = gw2[t][4][r];  // b2 (every column of the ones tile holds it)
-      }
-    // head weights: ghw[t] rows d = 4 lk + r (lk == 0: d = r), columns = units 16 t + li
-    if (lk == 0) {
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        r2[(16 * t + li) * VR + 65] = ghw[t][0];
-        r2[(16 * t + li) * VR + 66] = ghw[t][1];
-      }
-    }
-    // scalar sums (head bias, log_std): over the wave's lanes, then into the last four words
-    sab0 = wave_sum(sab0);
-    sab1 = wave_sum(sab1);
-    slg0 = wave_sum(slg0);
-    slg1 = wave_sum(slg1);
-    la = wave_sum(la);
-    lb = wave_sum(lb);
-    lc = wave_sum(lc);
-    ln = wave_sum(ln);
-    float* sc = tl + 4 * 64 * VR;
-    if (lane == 0) {
-      sc[8 * wave + 0] = sab0;
-      sc[8 * wave + 1] = sab1;
-      sc[8 * wave + 2] = slg0;
-      sc[8 * wave + 3] = slg1;
-      sc[8 * wave + 4] = la;
-      sc[8 * wave + 5] = lb;
-      sc[8 * wave + 6] = lc;
-      sc[8 * wave + 7] = ln;
-    }
-    __syncthreads();
-    for (int i = lane; i < 16 * VR; i += 64) {
-      const int u = 16 * wave + i / VR, k = i % VR, o = u * VR + k;
-      if (net && k == 66) continue;  // the critic has one head row
-      const float s = (tl[o] + tl[64 * VR + o]) + (tl[2 * 64 * VR + o] + tl[3 * 64 * VR + o]);
-      if (k < 64) g[ow2 + u * H + k] = s;
-      else if (k == 64) g[ob2 + u] = s;
-      else g[ohw + (k - 65) * H + u] = s;
-    }
-    if (tid < 8) {
-      const float s = (sc[tid] + sc[8 + tid]) + (sc[16 + tid] + sc[24 + tid]);
-      float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
-      if (net == 0) {
-        if (tid < 2) g[ACKPPO_OFF_ACT_B + tid] = s;
-        else if (tid < 4) g[ACKPPO_OFF_LOG_STD + tid - 2] = s;
-        else lp[tid == 4 ? 0 : tid - 3] = s;  // policy loss, clipped count, approx-kl sum, samples
-        if (tid == 0) lp[5] = lp[6] = lp[7] = 0.0f;
-      } else {
-        if (tid == 0) g[ACKPPO_OFF_VAL_B] = s;
-        if (tid == 4) lp[1] = s;  // value loss sum
-      }
-    }
-  }
-  PSTAMP(15);
-  PRSTAMP(14);
-}
-extern "C" __global__ void __launch_bounds__(GRAD_THREADS, 1) ackppo_grad2_kernel(GradArgs A) { grad2(A); }
-
 // ---- ackppo_act: MFMA policy tile. 16 envs per 256-lane workgroup (4096 envs = 256 workgroups,
 // one per CU): the weights are staged as in ackppo_grad (transposed / swizzled), X [80][16],
 // H1 / H2 [128 units][16 envs] in LDS; wave w computes unit tiles 2w, 2w + 1 of both layers as
@@ -1591,6 +1215,35 @@ extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_perm_stats_kern
   }
 }
 
+// The data-parallel form of ackppo_perm_stats_kernel: workgroup (m, e) writes positions
+// [m B, (m + 1) B) of epoch e's shuffle and this rank's (count, sum) of minibatch m's advantages
+// into moments[0..1][e][m] (ackppo_adv_moments_kernel phase 0's arithmetic, the same bits); one
+// all-reduce then covers every epoch's first moments.
+extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_perm_moments_kernel(const float* adv, int n, int batch,
+                                                                                     uint64_t seed, uint32_t epoch0,
+                                                                                     int32_t* perm, double* moments) {
+  __shared__ double red[ADV_THREADS / 64];
+  const int m = blockIdx.x, e = blockIdx.y, tid = threadIdx.x, nmb = gridDim.x, NM = nmb * gridDim.y;
+  const int j = e * nmb + m;
+  uint32_t keys[4];
+  perm_keys(seed, epoch0 + (uint32_t)e, keys);
+  const int half = perm_half(n);
+  int32_t* out = perm + (size_t)e * n;
+  const int lo = m * batch, hi = min(lo + batch, n), cnt = hi - lo;
+  double s = 0.0;
+  for (int i = lo + tid; i < hi; i += ADV_THREADS) {
+    const uint32_t x = perm_at((uint32_t)i, n, half, keys);
+    out[i] = (int32_t)x;
+    s += adv[x];
+  }
+  const double tot = block_sum_d(s, red);
+  if (tid == 0) {
+    moments[j] = (double)cnt;
+    moments[NM + j] = tot;
+    moments[2 * NM + j] = 0.0;
+  }
+}
+
 // Two passes, no atomics, no scratch: (1) grid (param blocks of 256, RG row groups) sums rows
 // by, by + RG, ... with 4 loads in flight per thread and writes the sum IN PLACE into row by
 // (row by belongs to group by alone, and element (by, p) to one thread, which read it first);
@@ -1810,12 +1463,7 @@ __device__ __forceinline__ void adam_block_update(const UpdArgs& A, int b, float
 // the partial rows reduced (8 row groups x 128 parameters; rows g, g + 8, ... in blocks of four as
 // ackppo_reduce1_kernel) into grad, the loss rows on workgroup 0, and S_b
 constexpr int RA_G = 8;
-// AK_PPO_RA_VEC: 16-B loads (a thread sums four adjacent parameters of its row group, 256 threads
-// per workgroup) -- per parameter the same rows in the same order as the scalar form (1024 threads)
-#ifndef AK_PPO_RA_VEC
-#define AK_PPO_RA_VEC 0
-#endif
-constexpr int RA_THREADS = AK_PPO_RA_VEC ? RA_G * NB_P / 4 : RA_G * NB_P;
+constexpr int RA_THREADS = RA_G * NB_P;
 __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P + 1], float* lred) {
   const int tid = threadIdx.x, b = blockIdx.x;
   const int pidx = b * NB_P + tid;  // threads 0-127: the parameter this thread finishes
@@ -1823,38 +1471,7 @@ __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P
   constexpr int RK = GRAD_MAX_BLOCKS / RA_G;
   static_assert(RK % 4 == 0, "row blocks of four");
   static_assert(P % 4 == 0 && NB_P % 4 == 0, "whole 16-B vectors per row and block");
-  if constexpr (AK_PPO_RA_VEC) {
-    const int pl4 = tid & (NB_P / 4 - 1), g = tid / (NB_P / 4);
-    const int vidx = b * (NB_P / 4) + pl4;
-    const bool vok = 4 * vidx < P;
-    float4 x[RK];
-#pragma unroll
-    for (int k = 0; k < RK; k++) {
-      const int r = g + k * RA_G;
-      // unconditional loads from valid addresses, zeros selected after (a conditional load compiles
-      // to an exec-masked branch that waits for it)
-      const float4 v = reinterpret_cast<const float4*>(A.gpart + (size_t)min(r, A.nblk - 1) * P)[min(vidx, P / 4 - 1)];
-      const bool ok = vok && r < A.nblk;
-      x[k] = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
-    }
-    int nmain = 0;
-#pragma unroll
-    for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < RK / 4; j++)
-        if (j < nmain) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) acc[i] += R1Vec<4>::at(x[4 * j + i], c);
-        }
-#pragma unroll
-      for (int k = 0; k < RK; k++)
-        if (k >= 4 * nmain) acc[0] += R1Vec<4>::at(x[k], c);
-      red[g][4 * pl4 + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    }
-  } else {
+  {
     const int pl = tid & (NB_P - 1), g = tid / NB_P;
     const int pcol = b * NB_P + pl;
     float x[RK];
@@ -1954,7 +1571,7 @@ int launched(const char* what) {
 #ifndef AK_GRAD1_LDS_PAD  // diagnostic builds: extra LDS per workgroup (e.g. one workgroup per CU)
 #define AK_GRAD1_LDS_PAD 0
 #endif
-constexpr size_t GRAD_LDS = (size_t)(AK_PPO_GRAD2 ? g2::TOTAL : g1::TOTAL) * sizeof(float) + AK_GRAD1_LDS_PAD;
+constexpr size_t GRAD_LDS = (size_t)g1::TOTAL * sizeof(float) + AK_GRAD1_LDS_PAD;
 // hipFuncSetAttribute is applied per device: flags indexed by the caller's current device
 constexpr int MAX_DEV = 64;
 bool g_grad_attr[MAX_DEV] = {};
@@ -1979,21 +1596,16 @@ bool g_grad1i_attr[MAX_DEV] = {};
 int grad_launch(const GradArgs& A, void* stream) {
   const int dev = current_device();
   if (dev < 0) return fail(ACKPPO_EHIP, "ackppo_grad: no usable current device");
-  const bool img = A.wimg != nullptr && !AK_PPO_GRAD2;
+  const bool img = A.wimg != nullptr;
   bool& ready = img ? g_grad1i_attr[dev] : g_grad_attr[dev];
   if (!ready) {
-    const void* kern = AK_PPO_GRAD2 ? (const void*)ackppo_grad2_kernel
-                                    : (img ? (const void*)ackppo_grad1i_kernel : (const void*)ackppo_grad1_kernel);
+    const void* kern = img ? (const void*)ackppo_grad1i_kernel : (const void*)ackppo_grad1_kernel;
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRAD_LDS) != hipSuccess)
       return fail(ACKPPO_EHIP, "ackppo_grad: cannot reserve the grad kernel's LDS footprint");
     ready = true;
   }
   const int nblk = ackppo_grad_blocks(A.batch);
-  if (AK_PPO_GRAD2)
-    hipLaunchKernelGGL(ackppo_grad2_kernel, dim3(2 * nblk), dim3(GRAD_THREADS),
-                       GRAD_LDS, (hipStream_t)stream, A);
-  else
-    hipLaunchKernelGGL(img ? ackppo_grad1i_kernel : ackppo_grad1_kernel, dim3(2 * nblk),
+  hipLaunchKernelGGL(img ? ackppo_grad1i_kernel : ackppo_grad1_kernel, dim3(2 * nblk),
                        dim3(GRAD_THREADS * g1::NT),
                        GRAD_LDS, (hipStream_t)stream, A);
   return launched("ackppo_grad");
@@ -2133,8 +1745,8 @@ int ackppo_grad(const float* params, const float* obs_rows, const float* actions
 
 int ackppo_grad_blocks(int batch) {
   if (batch <= 0) return 0;
-  const int tiles = (batch + (AK_PPO_GRAD2 ? g2::T : g1::T) - 1) / (AK_PPO_GRAD2 ? g2::T : g1::T);
-  const int rows = AK_PPO_GRAD2 ? tiles : (tiles + g1::NT - 1) / g1::NT;  // one partial row per tile group
+  const int tiles = (batch + g1::T - 1) / g1::T;
+  const int rows = (tiles + g1::NT - 1) / g1::NT;  // one partial row per tile group
   return rows < GRAD_MAX_BLOCKS ? rows : GRAD_MAX_BLOCKS;
 }
 
@@ -2231,7 +1843,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
   const bool dp = d->allreduce != nullptr;
   if ((d->world > 1 && !dp) || (dp && !d->moments))
     return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
-  float* wimg = AK_PPO_GRAD2 ? nullptr : d->weight_image;
+  float* wimg = d->weight_image;
   const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
@@ -2253,13 +1865,30 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     }
     return ACKPPO_OK;
   };
-  // single rank with the per-call buffers: every epoch's shuffle and statistics in one launch now
-  const bool all_epochs = !dp && d->perm_epochs && d->stats_epochs;
+  // with the per-call buffers: every epoch's shuffle and statistics at the start (the advantages do
+  // not change during the call) -- single rank one launch; data-parallel the shuffles and first
+  // moments in one launch, 2 all-reduces for all epochs (not 2 per epoch), deviations, finalize
+  const bool all_epochs = d->perm_epochs && d->stats_epochs;
   if (all_epochs) {
     if (S > (1 << 30)) return fail(ACKPPO_EINVAL, "ackppo_train: n_idx too large for the shuffle");
-    hipLaunchKernelGGL(ackppo_perm_stats_kernel, dim3(nmb, d->n_epochs), dim3(ADV_THREADS), 0, st, d->advantages, S, B,
-                       d->perm_key, d->perm_epoch0, d->normalize_advantage, d->perm_epochs, d->stats_epochs);
-    if ((rc = launched("ackppo_train: shuffles and statistics"))) return rc;
+    const dim3 grid(nmb, d->n_epochs);
+    if (!dp) {
+      hipLaunchKernelGGL(ackppo_perm_stats_kernel, grid, dim3(ADV_THREADS), 0, st, d->advantages, S, B, d->perm_key,
+                         d->perm_epoch0, d->normalize_advantage, d->perm_epochs, d->stats_epochs);
+      if ((rc = launched("ackppo_train: shuffles and statistics"))) return rc;
+    } else {
+      const int NM = nmb * d->n_epochs;
+      double* mom = d->moments;
+      hipLaunchKernelGGL(ackppo_perm_moments_kernel, grid, dim3(ADV_THREADS), 0, st, d->advantages, S, B, d->perm_key,
+                         d->perm_epoch0, d->perm_epochs, mom);
+      if ((rc = launched("ackppo_train: shuffles and moments"))) return rc;
+      if ((rc = coll(mom, 2 * (int64_t)NM, ACKPPO_F64, "advantage count/sum"))) return rc;
+      hipLaunchKernelGGL(ackppo_adv_moments_kernel, grid, dim3(ADV_THREADS), 0, st, d->advantages, d->perm_epochs, S,
+                         B, 1, nmb, mom);
+      if ((rc = launched("ackppo_train: advantage deviations"))) return rc;
+      if ((rc = coll(mom + 2 * NM, NM, ACKPPO_F64, "advantage deviation"))) return rc;
+      if ((rc = ackppo_adv_finalize(mom, NM, d->normalize_advantage, d->stats_epochs, stream))) return rc;
+    }
   }
   UpdArgs U{d->grad_partial, 0, d->loss_partial, d->ent_coef, d->grad, d->loss_acc, 1, 1, d->params, d->exp_avg,
             d->exp_avg_sq, 1.0f / (float)d->world, d->max_grad_norm, (float)d->beta1, (float)d->beta2, d->eps, 0.0f,
@@ -2270,7 +1899,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     if (!all_epochs && !dp) {
       if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
       if ((rc = ackppo_adv_stats(d->advantages, d->perm, S, B, d->normalize_advantage, d->stats, stream))) return rc;
-    } else if (dp) {
+    } else if (dp && !all_epochs) {
       if ((rc = ackppo_permutation(S, d->perm_key, d->perm_epoch0 + (uint32_t)ep, d->perm, stream))) return rc;
       double* mom = d->moments;
       if ((rc = ackppo_adv_moments(d->advantages, d->perm, S, B, 0, mom, stream))) return rc;
@@ -2318,9 +1947,9 @@ struct Rccl {
 Rccl& rccl() {
   static Rccl r = [] {
     Rccl x;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // already in the process (torch)
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    // only the RCCL already in the process (torch's): a second copy, built against another HIP
+    // runtime, must never be loaded beside it (its communicators would not be torch's either)
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
     if (!h) return x;
     x.get_id = (decltype(x.get_id))dlsym(h, "ncclGetUniqueId");
     x.init = (decltype(x.init))dlsym(h, "ncclCommInitRank");
@@ -2340,7 +1969,7 @@ int rccl_fail(const char* what, ncclResult_t r) {
 
 int ackppo_rccl_unique_id(void* id128) {
   if (!id128) return fail(ACKPPO_EINVAL, "ackppo_rccl_unique_id: bad arguments");
-  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_unique_id: librccl.so.1 not loadable");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_unique_id: no librccl.so.1 loaded in this process (import torch first)");
   static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
   ncclUniqueId id;
   const ncclResult_t r = rccl().get_id(&id);
@@ -2352,7 +1981,7 @@ int ackppo_rccl_unique_id(void* id128) {
 int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm) {
   if (!id128 || !comm || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(ACKPPO_EINVAL, "ackppo_rccl_init: bad arguments");
-  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_init: librccl.so.1 not loadable");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_init: no librccl.so.1 loaded in this process (import torch first)");
   ncclUniqueId id;
   memcpy(&id, id128, sizeof id);
   ncclComm_t c = nullptr;
@@ -2365,6 +1994,7 @@ int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm) {
 int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void* stream) {
   if (!buf || !comm || count < 0 || (dtype != ACKPPO_F32 && dtype != ACKPPO_F64))
     return fail(ACKPPO_EINVAL, "ackppo_rccl_allreduce: bad arguments");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_allreduce: no librccl.so.1 loaded in this process");
   const ncclResult_t r = rccl().allreduce(buf, buf, (size_t)count, dtype == ACKPPO_F32 ? ncclFloat32 : ncclFloat64,
                                           ncclSum, (ncclComm_t)comm, (hipStream_t)stream);
   return r == ncclSuccess ? ACKPPO_OK : rccl_fail("ncclAllReduce", r);
@@ -2372,9 +2002,20 @@ int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void*
 
 int ackppo_rccl_destroy(void* comm) {
   if (!comm) return ACKPPO_OK;
-  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_destroy: librccl.so.1 not loadable");
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_destroy: no librccl.so.1 loaded in this process");
   const ncclResult_t r = rccl().destroy((ncclComm_t)comm);
   return r == ncclSuccess ? ACKPPO_OK : rccl_fail("ncclCommDestroy", r);
+}
+
+int ackppo_rccl_library(char* path, int size) {
+  if (!path || size <= 0) return fail(ACKPPO_EINVAL, "ackppo_rccl_library: bad arguments");
+  path[0] = 0;
+  if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_library: no librccl.so.1 loaded in this process");
+  Dl_info info;
+  if (!dladdr((void*)rccl().allreduce, &info) || !info.dli_fname)
+    return fail(ACKPPO_EHIP, "ackppo_rccl_library: dladdr failed");
+  snprintf(path, (size_t)size, "%s", info.dli_fname);
+  return ACKPPO_OK;
 }
 
 }  // extern "C"

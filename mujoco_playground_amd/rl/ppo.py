@@ -23,8 +23,8 @@ statistics of all world x batch_size samples (ackppo_adv_moments: two small all-
 per-minibatch count / sum / squared deviations per epoch), as one SB3 learner would. The
 collectives are enqueued from C by ackppo_train through a hook (shard.TrainerCollective): a native
 RCCL communicator (ackppo_rccl_allreduce) on GPU nodes, a host-staged torch.distributed callback in
-gloo rehearsals -- per iteration n_epochs x (nmb + 2) all-reduces, none of them a host round trip
-on the RCCL path.
+gloo rehearsals -- per iteration n_epochs x nmb + 2 all-reduces (the advantage moments of every
+epoch formed at the start of train()), none of them a host round trip on the RCCL path.
 """
 from __future__ import annotations
 
@@ -172,18 +172,20 @@ class PPO:
         self.gnorm = torch.zeros(1, **f32)
         nmb = (T * N + batch_size - 1) // batch_size
         self.mb_stats = torch.zeros(nmb, 2, **f32)
-        self.mb_moments = torch.zeros(3, nmb, dtype=torch.float64, device=dev)  # DP advantage statistics
+        # DP advantage statistics: [3][n_epochs][nmb] (all epochs at the start of train(); the per-epoch
+        # path uses its first [3][nmb] words)
+        self.mb_moments = torch.zeros(3, n_epochs * nmb, dtype=torch.float64, device=dev)
         # per-epoch minibatch shuffle: ackppo_permutation keyed by (seed, rank) and the epoch count
         self.perm_key = (self.seed * 7919 + self.rank) & 0xFFFFFFFFFFFFFFFF
         self.perm_epoch = 0
         self.perm = torch.empty(self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
-        # every epoch's shuffle and statistics of one train() call, formed by one launch at its start
-        # (ackppo_train_desc perm_epochs / stats_epochs; the data-parallel path keeps per-epoch launches)
+        # every epoch's shuffle and statistics of one train() call, formed at its start (ackppo_train_desc
+        # perm_epochs / stats_epochs: one launch single-rank; 2 all-reduces per call data-parallel)
         self.perm_epochs = torch.empty(self.n_epochs, self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
         self.stats_epochs = torch.zeros(self.n_epochs, nmb, 2, **f32)
-        # the all-reduce hook of the data-parallel update: RCCL (native communicator) on GPU nodes,
-        # host-staged in gloo rehearsals; collective="rccl" at world 1 runs the data-parallel path over
-        # a one-rank communicator (timing that path on one GPU)
+        # the all-reduce hook of the data-parallel update (shard.TrainerCollective): on GPU nodes RCCL on
+        # torch's own communicator ("torch", the default) or on libackppo's ("rccl", opt-in); host-staged in
+        # gloo rehearsals; a kind at world 1 runs the data-parallel path over one rank (timing it on one GPU)
         self.collective = None
         self._desc = self._train_desc()
         if self.world > 1 or collective is not None:
@@ -324,8 +326,8 @@ class PPO:
         d.weight_image = self.weight_image.data_ptr() if on else None
 
     def set_collective(self, kind: str | None):
-        """The update's all-reduce hook (shard.TrainerCollective): "rccl", "host", None = the
-        backend's default at world > 1, or no hook at all at world 1."""
+        """The update's all-reduce hook (shard.TrainerCollective): "torch", "rccl", "host", None = the
+        backend's default at world > 1 ("torch" on RCCL, "host" on gloo), or no hook at all at world 1."""
         if self.collective is not None:
             self.collective.close()
             self.collective = None
@@ -335,8 +337,12 @@ class PPO:
             return
         c = shard.TrainerCollective(self.world, self.device, kind=kind)
         c.register(self.grad)
-        c.register(self.mb_moments[0:2].reshape(-1))
-        c.register(self.mb_moments[2])
+        flat = self.mb_moments.view(-1)
+        nm, nmb = self.mb_moments.shape[1], self.mb_moments.shape[1] // self.n_epochs
+        c.register(flat[0:2 * nm])              # all-epoch moments: (count, sum) rows, then deviations
+        c.register(flat[2 * nm:3 * nm])
+        c.register(flat[0:2 * nmb])             # per-epoch layout [3][nmb] (set_epoch_buffers(False))
+        c.register(flat[2 * nmb:3 * nmb])
         self.collective = c
         d.allreduce, d.allreduce_user = c.fn.value, c.user
 

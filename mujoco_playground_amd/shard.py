@@ -96,19 +96,53 @@ def all_reduce_sum_(t: torch.Tensor, world: int) -> torch.Tensor:
     return t
 
 
+def _abort_group():
+    """Tear the default process group down after a local collective error, so the other ranks'
+    pending collectives fail (connection closed / communicator aborted) instead of waiting forever
+    for this rank -- a local error must not become a distributed hang."""
+    try:
+        from torch.distributed import distributed_c10d as c10d
+        if hasattr(c10d, "_abort_process_group"):
+            c10d._abort_process_group()
+        else:
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001 -- best effort on an already failing path
+        pass
+
+
+def torch_rccl_comm(device) -> int:
+    """The ncclComm_t of torch's ProcessGroupNCCL for `device` (the communicator the default process
+    group built and already uses for every other collective of the run). One all-reduce first, so
+    the communicator exists (torch creates it lazily on the first collective of the device)."""
+    with torch.cuda.device(device):
+        t = torch.zeros(1, device=device)
+        dist.all_reduce(t)
+        torch.cuda.synchronize(device)
+        backend = dist.distributed_c10d._get_default_group()._get_backend(torch.device("cuda", device.index))
+        ptr = int(backend._comm_ptr())
+    if not ptr:
+        raise RuntimeError("torch's ProcessGroupNCCL has no communicator for this device")
+    return ptr
+
+
 class TrainerCollective:
     """The all-reduce hook libackppo's ackppo_train calls between a minibatch's gradient and its Adam
     step (include/ackppo.h ackppo_allreduce_fn), so a data-parallel PPO update is one C call per
     train() with no per-minibatch host round trip.
 
-    kind "rccl": a native RCCL communicator of libackppo (ackppo_rccl_*) over the ranks of the
+    kind "torch" (default on the nccl = RCCL backend): ackppo_rccl_allreduce on the communicator of
+      torch's own ProcessGroupNCCL (torch_rccl_comm): no second communicator, no unique-id exchange,
+      and the RCCL library is checked to be the one torch loaded; each collective is enqueued from C
+      on the trainer's stream (torch's current stream, so torch's later collectives on the same
+      communicator are ordered after them on the device).
+    kind "rccl" (opt-in): a communicator of libackppo's own (ackppo_rccl_*) over the ranks of the
       default process group (its unique id broadcast once over that group), or over this process
       alone at world 1 (a one-rank communicator: the data-parallel path with real RCCL calls, for
-      timing it on one GPU); the hook is ackppo_rccl_allreduce itself, so each collective is
-      enqueued from C.
+      timing it on one GPU).
     kind "host": a Python callback that all-reduces through torch.distributed on host copies --
       the gloo rehearsals (several ranks on one device, where RCCL cannot run); the callback
-      synchronises the stream, so it is the slow path, for tests only.
+      synchronises the stream, so it is the slow path, for tests only. On an error it aborts the
+      process group, so the other ranks fail too rather than wait.
     Buffers handed to the "host" hook must be registered (`register`)."""
 
     def __init__(self, world: int, device, kind: str | None = None):
@@ -116,11 +150,23 @@ class TrainerCollective:
 
         from . import _lib
         self.world, self.device = world, device
-        self.kind = kind or ("host" if _backend_is_gloo() else "rccl")
+        self.kind = kind or ("host" if _backend_is_gloo() else "torch")
         self.L = _lib.ppo_lib()
         self._bufs = {}
         self.comm = C.c_void_p()
-        if self.kind == "rccl":
+        if self.kind in ("torch", "rccl"):
+            path = C.create_string_buffer(4096)
+            _lib.ppo_check(self.L.ackppo_rccl_library(path, 4096), "ackppo_rccl_library")
+            self.library = path.value.decode()
+        if self.kind == "torch":
+            if not (dist.is_initialized() and dist.get_backend() == "nccl"):
+                raise RuntimeError('collective "torch" needs the default process group on the nccl (RCCL) backend')
+            torch_lib = _torch_rccl_path()
+            if torch_lib is not None and os.path.realpath(torch_lib) != os.path.realpath(self.library):
+                raise RuntimeError(f"libackppo resolved RCCL at {self.library}, torch's is {torch_lib}")
+            self.user = C.c_void_p(torch_rccl_comm(device))
+            self.fn = C.cast(self.L.ackppo_rccl_allreduce, C.c_void_p)
+        elif self.kind == "rccl":
             idb = (C.c_char * 128)()
             rank = dist.get_rank() if world > 1 else 0
             if rank == 0:
@@ -139,7 +185,9 @@ class TrainerCollective:
                     all_reduce_sum_(t, self.world)
                     return 0
                 except Exception as e:  # noqa: BLE001 -- reported through the C return code
-                    print(f"TrainerCollective host hook: {e!r}", flush=True)
+                    print(f"TrainerCollective host hook: {e!r}; aborting the process group", flush=True)
+                    if self.world > 1:
+                        _abort_group()
                     return -1
             self._cb = _lib.ALLREDUCE_FN(hook)  # kept alive with the collective
             self.fn = C.cast(self._cb, C.c_void_p)
@@ -162,6 +210,18 @@ class TrainerCollective:
             self.close()
         except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
+
+
+def _torch_rccl_path():
+    """Path of the librccl mapped into this process by torch (None if it cannot be told)."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "librccl" in line:
+                    return line.split()[-1]
+    except OSError:
+        pass
+    return None
 
 
 def broadcast_(t: torch.Tensor, world: int, src: int = 0) -> torch.Tensor:

@@ -219,10 +219,11 @@ def _horizontal(before_e, ray, g, r):
     return abs(d[2]) <= HORIZ_TOL * np.linalg.norm(d) and abs(pair[0] + 1.0) <= 1e-6 and abs(pair[1] - 12.0) <= 1e-4
 
 
-def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None, excuse=None):
+def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None, excuse=None, on_step=None):
     """obs_pose(before, actions) -> the states the observations are taken at (default: `before`, the
     pre-integration pose; with action_repeat R, the pose after R-1 mj_steps). excuse(k, e, before_e,
-    act_e, after_e) replaces the boundary excuse (default: _excused with the oracle `o`)."""
+    act_e, after_e) replaces the boundary excuse (default: _excused with the oracle `o`).
+    on_step(k, ref, after, ok, oterm, otr, tobs): extra per-step checks."""
     worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0, excused=0, grazing_rays=0, rays=0)
     for k in range(steps):
         before = f64_state(sim.state)
@@ -232,7 +233,7 @@ def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None, excu
         after = f64_state(sim.state)
         ref = before.copy()
         a_np = acts[k].cpu().numpy()
-        oobs, orew, oterm, otr, _, _ = o.step(ref, a_np, flags=flags, seed=seed, terminal=True)
+        oobs, orew, oterm, otr, tobs, _ = o.step(ref, a_np, flags=flags, seed=seed, terminal=True)
         dq = np.abs(after[:, :13] - ref[:, :13]).max(axis=1)
         dv = np.abs(after[:, 13:25] - ref[:, 13:25]).max(axis=1)
         ok = (dq <= TOL_QPOS) & (dv <= TOL_QVEL)
@@ -266,6 +267,8 @@ def teacher_forced(sim, o, acts, steps, flags, seed, lo, hi, obs_pose=None, excu
         assert dr <= TOL_REW
         np.testing.assert_array_equal(sim.term.cpu().numpy().astype(bool)[ok], oterm[ok])
         np.testing.assert_array_equal(sim.trunc.cpu().numpy().astype(bool)[ok], otr[ok])
+        if on_step is not None:
+            on_step(k, ref, after, ok, oterm, otr, tobs)
     assert worst["excused"] <= 5e-3 * steps * sim.n, worst
     assert worst["grazing_rays"] <= 1e-3 * worst["rays"], worst
     return worst

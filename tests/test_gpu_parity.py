@@ -78,7 +78,9 @@ def _boundary_excused(o, before_e, act_e, after_e, flags, seed):
     return False
 
 
-def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
+def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True, on_step=None):
+    """Every step from the GPU's own state, against the oracle (tolerances above; boundary excuses
+    counted and capped). on_step(k, ref, after, ok, oterm, otr, tobs): extra per-step checks."""
     worst = dict(qpos=0.0, qvel=0.0, obs=0.0, rew=0.0, excused=0, excused_rays=0)
     for k in range(steps):
         before = f64_state(sim.state)
@@ -100,6 +102,8 @@ def teacher_forced(sim, o, acts, steps, flags, seed, check_obs=True):
         np.testing.assert_array_equal(sim.term.cpu().numpy().astype(bool)[ok], oterm[ok])
         np.testing.assert_array_equal(sim.trunc.cpu().numpy().astype(bool)[ok], otr[ok])
         np.testing.assert_array_equal(after[ok, 42:44], ref[ok, 42:44])
+        if on_step is not None:
+            on_step(k, ref, after, ok, oterm, otr, tobs)
         if check_obs:
             gobs = sim.obs_soa.cpu().numpy().T
             do = np.abs(gobs - oobs) / (1.0 + 0.1 * np.abs(oobs))

@@ -5,7 +5,11 @@ against the f64 CPU oracle (both sides start each step from the same GPU state).
   configs[1] (contacts off)   steps 0-50 from reset (the bench's headline workload);
   configs[2] (contacts on)    steps 200-300, after the bench's 200 settle steps (one rollout launch,
                               bit-identical to per-step launches: tests/test_gpu_rollout.py);
-  obstacle scene (configs[4]'s world)  the same window.
+  obstacle scene (configs[4]'s world)  the same window;
+  the episode boundary, both scenes   steps 990-1010 (ackermann_env.py:216-220 truncation at 1000,
+                              then the auto-reset of :143-185): step counter, truncation, the
+                              terminal observation, the reset state with its Philox goal redraw and
+                              odometry reference, and the reset observation, all against the oracle.
 
 Tolerances and boundary excuses are those of tests/test_gpu_parity.py (flat scene) and
 tests/test_gpu_obstacles.py (obstacle scene); here every excused env-step is counted, reported and
@@ -80,3 +84,42 @@ def _boxes(sblob):
     c = np.array([list(h.geom_pos[i]) for i in g])
     s = np.array([list(h.geom_size[i]) for i in g])
     return c - s, c + s
+
+
+def _boundary_checks(sim, tol_obs):
+    """on_step checks of the episode-boundary windows: the auto-reset state words the generic
+    comparison does not cover (goal 37-38 drawn from Philox keyed (env, episode), odometry
+    reference 39-41) and the terminal observation of every env that reset."""
+    seen = {"resets": 0}
+
+    def check(k, ref, after, ok, oterm, otr, tobs):
+        done = ok & (oterm | otr)
+        seen["resets"] += int(done.sum())
+        np.testing.assert_allclose(after[ok, 37:42], ref[ok, 37:42], rtol=1e-6, atol=1e-6)
+        if done.any():
+            gt = sim.terminal_obs_soa.cpu().numpy().T
+            d = np.abs(gt[done] - tobs[done]) / (1.0 + 0.1 * np.abs(tobs[done]))
+            ray_pair = np.isin(gt[done], (-1.0, 12.0)) & np.isin(tobs[done], (-1.0, 12.0))  # ray-horizon pairs
+            assert (d[~ray_pair] <= tol_obs).all(), f"step {k}: terminal obs {d[~ray_pair].max()}"
+    return check, seen
+
+
+@pytest.mark.parametrize("scene", ["flat", "obstacles"])
+def test_episode_boundary_steps_990_1010(blob, scene):
+    """The step-1000 truncation -> auto-reset -> terminal observation -> goal redraw boundary at the
+    BASELINE size, teacher-forced against the oracle: every env truncates at
+    step 1000 of its first episode unless it terminated earlier."""
+    from mujoco_playground_amd import _lib
+    K0, W = 990, 20
+    sblob = blob if scene == "flat" else _lib.load_blob("obstacles")
+    sim = _bench_sim(True, scene=scene)
+    acts = sim.random_actions(K0 + W, seed=SEED)
+    sim.rollout(acts[:K0], want_info=False, per_step_outputs=False)
+    check, seen = _boundary_checks(sim, TP.TOL_OBS)
+    if scene == "flat":
+        w = TP.teacher_forced(sim, TP.fresh_oracle(sblob), acts[K0:], W, 3, SEED, on_step=check)
+    else:
+        lo, hi = _boxes(sblob)
+        w = TO.teacher_forced(sim, TO.oracle(sblob), acts[K0:], W, 3, SEED, lo, hi, on_step=check)
+    assert seen["resets"] >= N // 2, seen  # the boundary really was crossed inside the window
+    _report(f"{scene} scene, episode boundary steps 990-1010", dict(w, resets=seen["resets"]), W)

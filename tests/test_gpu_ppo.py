@@ -321,25 +321,88 @@ def test_adv_moments_two_ranks_normalise_the_world_minibatch():
 
 
 def test_train_paths_bit_identical():
-    """PPO.train is one ackppo_train call. Its single-rank sequence (no hook), the data-parallel
-    sequence over a one-rank native RCCL communicator (ackppo_rccl_allreduce: the world > 1 path with
-    real RCCL calls) and over the host-staged hook (the gloo rehearsals' path, a no-op at world 1)
-    give bit-identical parameters, Adam moments and loss statistics: the single-rank reduction +
-    Adam launch and the data-parallel reduction -> all-reduce -> Adam launches share their order."""
+    """PPO.train is one ackppo_train call. Its single-rank sequence (no hook) and the data-parallel
+    sequence over one rank -- RCCL on torch's own communicator (kind "torch", the default at world > 1;
+    a one-rank nccl process group here), on libackppo's own communicator ("rccl") and the host-staged
+    hook (the gloo rehearsals' path, a no-op at world 1), each with every epoch's advantage moments
+    formed at the start of the call (2 collectives per call) and with per-epoch moments -- give
+    bit-identical parameters, Adam moments and loss statistics."""
+    import torch.distributed as dist
     from mujoco_playground_amd.rl import make_ackermann_env
     from mujoco_playground_amd.rl.ppo import PPO
+    made = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device(DEV))
+        made = True
     out = []
-    for coll in (None, "rccl", "host"):
-        venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
-        model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01, collective=coll)
-        assert (model.collective is None) == (coll is None)
-        model.learn(total_timesteps=2 * 16 * 256)
-        out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
-                    model.logger["train/value_loss"], model.logger["train/approx_kl"]))
+    try:
+        for coll, epochs_buf in ((None, True), ("torch", True), ("torch", False), ("rccl", True), ("rccl", False),
+                                 ("host", True), ("host", False)):
+            venv = make_ackermann_env(env_type="vec", num_envs=256, max_episode_steps=64, device=DEV)
+            model = PPO("MlpPolicy", venv, n_steps=16, batch_size=1000, n_epochs=3, seed=7, ent_coef=0.01,
+                        collective=coll)
+            model.set_epoch_buffers(epochs_buf)
+            assert (model.collective is None) == (coll is None)
+            model.learn(total_timesteps=2 * 16 * 256)
+            out.append((model.params.cpu().numpy(), model.exp_avg_sq.cpu().numpy(), model.adam_step,
+                        model.logger["train/value_loss"], model.logger["train/approx_kl"]))
+            if coll is not None:
+                model.set_collective(None)
+    finally:
+        if made:
+            dist.destroy_process_group()
     for o in out[1:]:
         np.testing.assert_array_equal(out[0][0], o[0])
         np.testing.assert_array_equal(out[0][1], o[1])
         assert out[0][2:] == o[2:]
+
+
+def _ppo_rank_rccl(rank, world, port, kind, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    from mujoco_playground_amd import shard
+    from mujoco_playground_amd.rl import AckermannVecEnv
+    from mujoco_playground_amd.rl.ppo import PPO
+    if kind == "host":
+        shard.init(backend="gloo")
+    else:
+        shard.init(backend="nccl")
+    dev = shard.device_for(rank) if kind != "host" else torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    venv = AckermannVecEnv(128, device=dev, seed=0, contacts=True, env_offset=shard.env_offset(rank, 128))
+    model = PPO("MlpPolicy", venv, n_steps=8, batch_size=256, n_epochs=2, seed=rank + 1,
+                collective=None if kind == "host" else kind)
+    model.learn(total_timesteps=2 * 8 * 128 * world)
+    q.put((rank, model.params.cpu().numpy(), model.adam_step))
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs 2 GPUs")
+def test_ppo_data_parallel_rccl_two_gpus():
+    """Two ranks on two GPUs over RCCL (torch's communicator, the default; and libackppo's own): both
+    ranks end with bit-identical parameters, equal to the host-hook (gloo) result of the same run."""
+    import socket
+    import torch.multiprocessing as mp
+    res = {}
+    for kind in ("host", "torch", "rccl"):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_ppo_rank_rccl, args=(r, 2, port, kind, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        got = sorted((q.get(timeout=300) for _ in ps), key=lambda t: t[0])
+        for p in ps:
+            p.join(timeout=60)
+        assert np.array_equal(got[0][1], got[1][1]), kind
+        res[kind] = got[0][1]
+    np.testing.assert_array_equal(res["host"], res["torch"])
+    np.testing.assert_array_equal(res["host"], res["rccl"])
 
 
 def test_train_matches_epoch_calls():

@@ -1,6 +1,6 @@
 """Where a PPO update's time goes: one rollout (4096 envs x 32 steps), then PPO.train() timed with
 and without the all-epochs shuffle buffers and the weight image (event-timed, 3 calls each). Under
-`rocprofv3 --kernel-trace` (tools/gpu_r04f.sh) the kernel trace then gives each kernel's duration
+`rocprofv3 --kernel-trace` (tools/gpu_steps.sh prof) the kernel trace then gives each kernel's duration
 and the idle gaps between consecutive kernels (tools/probes/ppo_update_timeline.py --trace DIR).
 
     python tools/probes/ppo_update_timeline.py              (timing)
