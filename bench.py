@@ -452,6 +452,26 @@ def check_world(gpus: int, world: int, rank: int) -> str:
     return backend
 
 
+_JSON_OUT = None
+
+
+def quiet_stdout():
+    """Everything but the result line goes to stderr: libraries print to fd 1 on their own (RCCL's
+    version banner when a communicator is created, for one), and the driver parses this process's
+    stdout as ONE JSON line. fd 1 is pointed at stderr; the line is written to a dup of the original."""
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(line: dict):
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
 def main():
     argv = sys.argv[1:]
     ap = argparse.ArgumentParser()
@@ -484,6 +504,7 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(argv, a.gpus))  # before any GPU call in this process
+    quiet_stdout()
     rank, world, local = shard.init()
     backend = check_world(a.gpus, world, rank)
     if a.check_launch:
@@ -494,7 +515,7 @@ def main():
             dist.all_gather_object(got, rank)
             ranks = got
         if rank == 0:
-            print(json.dumps({"check_launch": True, "n_gpus": world, "ranks": ranks, "backend": backend}), flush=True)
+            emit({"check_launch": True, "n_gpus": world, "ranks": ranks, "backend": backend})
         if world > 1:
             torch.distributed.destroy_process_group()
         return
@@ -638,7 +659,7 @@ def main():
             "cpu_baseline": base, "parity": parity, "episodes": rets, "secondary": secondary, "ppo": ppo,
             "obstacles": obstacles,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         torch.distributed.destroy_process_group()
 

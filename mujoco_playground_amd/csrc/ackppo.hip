@@ -453,6 +453,7 @@ constexpr int TSZ = TOTAL1 - WEND;  // one tile's region (X .. GA)
 #ifndef AK_GRAD1_PREFETCH
 #define AK_GRAD1_PREFETCH 0
 #endif
+
 constexpr int NT = AK_GRAD1_NT;
 static_assert(NT == 1 || NT == 2, "one or two tiles per workgroup");
 constexpr int TOTAL = WEND + NT * TSZ;
@@ -680,8 +681,14 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
   // overlaps it; the registers they hold through the staging cost a few spill slots)
   if (AK_GRAD1_PREFETCH && grp0 < ngrp) loads(NT * grp0 + half);
-  if constexpr (IMG) stage_image<NTHR>(A.wimg + net * WIMG, w);
-  else stage_net<L1, NTHR>(A.params, w, net);
+  if constexpr (IMG) {
+    stage_image<NTHR>(A.wimg + net * WIMG, w);
+    // the LDS-DMA copies count in vmcnt, not lgkmcnt: drain them before the first barrier makes the
+    // block visible to the other waves (on gfx950 neither the barrier nor a workgroup fence waits)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    stage_net<L1, NTHR>(A.params, w, net);
+  }
 
   f4v gw1[5], gw2[4];
 #pragma unroll

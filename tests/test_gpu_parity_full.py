@@ -95,7 +95,7 @@ def _boundary_checks(sim, tol_obs):
     def check(k, ref, after, ok, oterm, otr, tobs):
         done = ok & (oterm | otr)
         seen["resets"] += int(done.sum())
-        np.testing.assert_allclose(after[ok, 37:42], ref[ok, 37:42], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(after[ok, 37:42], ref[ok, 37:42], rtol=1e-6, atol=1e-5)  # f32 goals: ~6 ulp at 8 m
         if done.any():
             gt = sim.terminal_obs_soa.cpu().numpy().T
             d = np.abs(gt[done] - tobs[done]) / (1.0 + 0.1 * np.abs(tobs[done]))

@@ -13,6 +13,7 @@
 #   kbench             tools/ppo_kbench.py
 #   quad=LIB:EPW,...   tools/probes/quad_time.py over step-library builds (diag_libs/*.so)
 #   stamps=ARGS        tools/stamps.py ARGS (comma-separated)
+#   stalls[=RUNS]      tools/profile_stalls.py (SQ wait / issue counters of the rollout kernels)
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -44,6 +45,7 @@ for step in "$@"; do
     kbench) run kbench 600 python3 tools/ppo_kbench.py ${val//,/ } ;;
     quad) run quad 900 python3 -u tools/probes/quad_time.py ${val//,/ } ;;
     stamps) run stamps 900 python3 -u tools/stamps.py ${val//,/ } ;;
+    stalls) run stalls 600 python3 -u tools/profile_stalls.py "$TAG" ${val//,/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -14,8 +14,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SQ = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
       "SQ_INSTS_VALU", "SQ_INSTS_SALU"]
-RUNS = [("lane_off", "ackphys_step_nc_kernel", ["--contacts", "0", "--variant", "lane"]),
-        ("quad_on", "ackphys_step_quad_kernel", ["--contacts", "1", "--variant", "quad"])]
+RUNS = [("lane_off", "ackphys_rollout_nc_kernel", ["--contacts", "0", "--variant", "lane"]),
+        ("quad_on", "ackphys_rollout_quad_kernel", ["--contacts", "1", "--variant", "quad"])]
+if len(sys.argv) > 2:  # e.g. quad_on only
+    RUNS = [r for r in RUNS if r[0] in sys.argv[2:]]
 
 
 def main():
@@ -26,7 +28,7 @@ def main():
         os.makedirs(out, exist_ok=True)
         cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *SQ, "--output-format", "csv", "-d", out, "-o",
                "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-secondary", "--no-ppo",
-               "--no-obstacles", "--steps", "40", "--warmup", "5", *extra]
+               "--no-obstacles", "--no-per-step", "--no-buffer-leg", "--steps", "200", "--warmup", "5", *extra]
         subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL)
         vals = {c: [] for c in SQ}
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):

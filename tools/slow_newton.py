@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--min-it", type=int, default=8)
     a = ap.parse_args()
-    L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", "libackphys_stamps.so"))
+    L = C.CDLL(os.path.join(REPO, "diag_libs", "libackphys_stamps.so"))
     P = C.c_void_p
     L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
     L.ackphys_step.argtypes = [P] * 10 + [C.c_uint32, C.c_uint64, P]

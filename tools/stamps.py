@@ -42,7 +42,7 @@ def main():
     quad = len(sys.argv) > 1 and sys.argv[1] in ("quad", "obst")
     obst = len(sys.argv) > 1 and sys.argv[1] == "obst"
     phases = QUAD_PHASES if quad else PHASES
-    L = C.CDLL(os.path.join(REPO, "mujoco_playground_amd", "csrc", "build", os.environ.get("DIAG_LIB", "libackphys_stamps.so")))
+    L = C.CDLL(os.path.join(REPO, "diag_libs", os.environ.get("DIAG_LIB", "libackphys_stamps.so")))
     P = C.c_void_p
     L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
     L.ackphys_step.argtypes = [P] * 10 + [C.c_uint32, C.c_uint64, P]
