@@ -168,6 +168,14 @@ struct Args {
   // the action alone) during step k from next_action into nctrl (LDS [3][64]); read when sm_in
   const float* next_action = nullptr;
   float* nctrl = nullptr;
+  // quad rollout kernels: where step k's observation wave writes step k + 1's controller output
+  // (the other half of a step-parity double buffer, so it can be written before barrier 1)
+  float* nctrl_out = nullptr;
+  // quad rollout kernels: LDS mirror of each env's step words ([8 envs][QSM_W]: qpos, qvel, warmstart,
+  // step, episode) written by the dynamics wave at the end of step k and read at the start of step k + 1
+  // instead of the HBM/L2 round trip (the state is still stored every step, for the observation wave)
+  float* qsm = nullptr;
+  int qsm_in = 0;
 #ifdef AK_STAMPS
   int stamp_skip = 0;  // diagnostic build: this role call's stamps are not flushed
 #endif
@@ -689,7 +697,10 @@ __device__ __forceinline__ void chol_sp_solve(const float H[NV][NV], float x[NV]
 #pragma unroll
   for (int i = 0; i < NV; i++) x[ORD[i]] = y[i];
 }
-// y = M x over the mass matrix's structural nonzeros (zero terms skipped, natural summation order)
+// y = M x over the mass matrix's structural nonzeros (zero terms skipped, natural summation order).
+// Entries that fold to a compile-time 0 (zero components of the model's constant axes and offsets)
+// are skipped too: IEEE keeps 0 * x (x may be inf), so the compiler emitted those multiplies; for
+// finite x a +-0 term never changes a sum that starts at +0.
 template <int KIND = 0>
 __device__ __forceinline__ void symv_M(const float M[NV][NV], const float x[NV], float y[NV]) {
 #pragma unroll
@@ -697,7 +708,10 @@ __device__ __forceinline__ void symv_M(const float M[NV][NV], const float x[NV],
     float s = 0;
 #pragma unroll
     for (int j = 0; j < NV; j++)
-      if (PAT[KIND].nz[i][j]) s += (j <= i ? M[i][j] : M[j][i]) * x[j];
+      if (PAT[KIND].nz[i][j]) {
+        const float m = j <= i ? M[i][j] : M[j][i];
+        if (!(__builtin_constant_p(m) && m == 0.0f)) s += m * x[j];
+      }
     y[i] = s;
   }
 }

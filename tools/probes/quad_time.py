@@ -41,7 +41,7 @@ def child(lib, steps, scene, contacts):
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) * 1e3 / steps)
     st = sim.state.double()
-    print(json.dumps({"lib": os.path.basename(lib), "epw": os.environ.get("ACKPHYS_QUAD_EPW", "8"),
+    print(json.dumps({"lib": os.path.basename(lib), "scene": scene, "epw": os.environ.get("ACKPHYS_QUAD_EPW", "8"),
                       "us_per_step": sorted(ts)[1], "all": ts, "checksum": float(st.abs().sum().item()),
                       "finite": bool(torch.isfinite(sim.state).all().item())}), flush=True)
 
@@ -50,7 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="*")
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--scene", default="flat")
+    ap.add_argument("--scene", default="flat", help="flat, obstacles or both")
     ap.add_argument("--contacts", type=int, default=1)
     ap.add_argument("--child", default=None)
     a = ap.parse_args()
@@ -63,12 +63,12 @@ def main():
         env = dict(os.environ)
         if epw:
             env["ACKPHYS_QUAD_EPW"] = epw
-        r = subprocess.run([sys.executable, __file__, "--child", lib, "--steps", str(a.steps), "--scene", a.scene,
-                            "--contacts", str(a.contacts)], env=env, timeout=300)
-        if r.returncode:
-            print(f"{spec}: exit {r.returncode}", flush=True)
-            rc = r.returncode
-            break
+        for scene in (("flat", "obstacles") if a.scene == "both" else (a.scene,)):
+            r = subprocess.run([sys.executable, __file__, "--child", lib, "--steps", str(a.steps), "--scene", scene,
+                                "--contacts", str(a.contacts)], env=env, timeout=300)
+            if r.returncode:
+                print(f"{spec}: exit {r.returncode}", flush=True)
+                sys.exit(r.returncode)
     sys.exit(rc)
 
 
