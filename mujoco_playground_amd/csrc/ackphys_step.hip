@@ -171,11 +171,6 @@ struct Args {
   // quad rollout kernels: where step k's observation wave writes step k + 1's controller output
   // (the other half of a step-parity double buffer, so it can be written before barrier 1)
   float* nctrl_out = nullptr;
-  // quad rollout kernels: LDS mirror of each env's step words ([8 envs][QSM_W]: qpos, qvel, warmstart,
-  // step, episode) written by the dynamics wave at the end of step k and read at the start of step k + 1
-  // instead of the HBM/L2 round trip (the state is still stored every step, for the observation wave)
-  float* qsm = nullptr;
-  int qsm_in = 0;
 #ifdef AK_STAMPS
   int stamp_skip = 0;  // diagnostic build: this role call's stamps are not flushed
 #endif

@@ -440,10 +440,14 @@ constexpr int W1T = 0, W2 = W1T + 80 * H, B1 = W2 + H * H, B2 = B1 + H;
 constexpr int HW = B2 + H;            // heads: actor [2][64] (critic [1][64])
 constexpr int HB = HW + 2 * H;        // actor: b[2], log_std[2] (critic: b[1])
 constexpr int WEND = HB + 4;
-constexpr int X = WEND, H1 = X + 80 * LDP, H2 = H1 + H * LDP, D2 = H2 + H * LDP;  // D1 overwrites H1
+// the tile regions start at TBASE = WEND rounded up to whole 64-lane float4 rounds (ACKPPO_WIMAGE):
+// the weight image's LDS-DMA copies (grad1i) write whole rounds, and their padding must not land in
+// a tile that another wave is already filling (the first tile's X is written before the barrier)
+constexpr int TBASE = (WEND + 255) / 256 * 256;
+constexpr int X = TBASE, H1 = X + 80 * LDP, H2 = H1 + H * LDP, D2 = H2 + H * LDP;  // D1 overwrites H1
 constexpr int GA = D2 + H * LDP;      // actor: gmu [2][LDP], glog [2][LDP]; critic: gv [LDP]
 constexpr int TOTAL1 = GA + 4 * LDP;
-constexpr int TSZ = TOTAL1 - WEND;  // one tile's region (X .. GA)
+constexpr int TSZ = TOTAL1 - TBASE;  // one tile's region (X .. GA)
 // NT tiles per workgroup (AK_GRAD1_NT): 1 = 256 threads, two workgroups per CU; 2 = 512 threads,
 // the two tiles' waves share one staged copy of the net's weights and one partial row (half the
 // rows for ackppo_reduce), one workgroup per CU
@@ -456,7 +460,7 @@ constexpr int TSZ = TOTAL1 - WEND;  // one tile's region (X .. GA)
 
 constexpr int NT = AK_GRAD1_NT;
 static_assert(NT == 1 || NT == 2, "one or two tiles per workgroup");
-constexpr int TOTAL = WEND + NT * TSZ;
+constexpr int TOTAL = TBASE + NT * TSZ;
 static_assert(NT == 2 ? TOTAL * 4 <= 160 * 1024 : TOTAL * 4 * 2 <= 160 * 1024,
               "two one-net grad workgroups (or one two-tile workgroup) per CU's 160 KiB LDS");
 // NT == 2: the end-of-kernel exchange of the halves' accumulators fits a tile region
@@ -467,7 +471,8 @@ constexpr int MAX_TILES = GRAD_MAX_BLOCKS;  // partial rows: one per tile (both 
 // the weight image (ackppo_train_desc::weight_image): net n's LDS weight block [0, WEND) at
 // n * WIMG, padded to whole 64-lane rounds of float4 copies
 constexpr int WIMG = ACKPPO_WIMAGE;
-static_assert(WEND <= WIMG && WIMG % 256 == 0 && WIMG - WEND < 256, "weight image: WEND in whole 64-lane float4 rounds");
+static_assert(WEND <= WIMG && WIMG % 256 == 0 && WIMG - WEND < 256 && WIMG == TBASE,
+              "weight image: WEND in whole 64-lane float4 rounds, the tiles after them");
 static_assert(WIMG <= TOTAL, "the image copy's padding lands inside the workgroup's LDS");
 // image position of parameter p (-1: a pad word); the inverse of stage_net's LDS map
 __device__ __forceinline__ int wimg_index(int p) {
@@ -650,19 +655,28 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   const int hs = 8 * wave + (lane & 7);
   float xg[10];
   float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  auto loads = [&](int tile) __attribute__((always_inline)) {
+  // a tile's gathers: the observation rows (X) and the heads' per-sample inputs (hin), each behind its
+  // sample-index load
+  auto row_idx = [&](int tile) __attribute__((always_inline)) {
+    const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
+    return A.idx[nvalid > 0 ? s0 + min(htid >> 3, nvalid - 1) : 0];
+  };
+  auto gather_x = [&](int tile, int ir) __attribute__((always_inline)) {
     // unconditional loads from valid addresses (a clamped sample and input), zeros selected after:
     // conditional loads compile to exec-masked branches that wait for each load in turn. A tile
     // past the batch (the second half of a last, odd group) has nvalid = 0: sample 0's rows, all zeroed
     const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
     const int r = htid >> 3, q = htid & 7;
-    const float* row = A.obs_rows + (size_t)A.idx[nvalid > 0 ? s0 + min(r, nvalid - 1) : 0] * NOBS;
+    const float* row = A.obs_rows + (size_t)ir * NOBS;
 #pragma unroll
     for (int i = 0; i < 10; i++) {
       const int k = q * 10 + i;
       const float v = row[min(k, NOBS - 1)];
       xg[i] = (r < nvalid && k < NOBS) ? v : 0.0f;
     }
+  };
+  auto gather_h = [&](int tile) __attribute__((always_inline)) {
+    const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
     const int sidx = A.idx[nvalid > 0 ? s0 + min(hs, nvalid - 1) : 0];
     const bool hv = hs < nvalid;
     if (net == 0) {
@@ -677,15 +691,32 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       hin[0] = hv ? rt : 0.0f;
     }
   };
+  auto loads = [&](int tile) __attribute__((always_inline)) {
+    gather_x(tile, row_idx(tile));
+    gather_h(tile);
+  };
 
   // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
   // overlaps it; the registers they hold through the staging cost a few spill slots)
-  if (AK_GRAD1_PREFETCH && grp0 < ngrp) loads(NT * grp0 + half);
+  if (AK_GRAD1_PREFETCH && !IMG && grp0 < ngrp) loads(NT * grp0 + half);
   if constexpr (IMG) {
+    // the first tile's sample indices, then the weight image's LDS-DMA copies (no registers), then the
+    // rows those indices address: the two dependent gathers run under the copies instead of after them
+    // (vmcnt retires in issue order, so the gathers' addresses wait only for the older index loads)
+    // (the heads' inputs are gathered in the loop: they are needed only after both layers)
+    int ir = 0;
+    if (grp0 < ngrp) ir = row_idx(NT * grp0 + half);
     stage_image<NTHR>(A.wimg + net * WIMG, w);
+    if (grp0 < ngrp) gather_x(NT * grp0 + half, ir);
     // the LDS-DMA copies count in vmcnt, not lgkmcnt: drain them before the first barrier makes the
     // block visible to the other waves (on gfx950 neither the barrier nor a workgroup fence waits)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (grp0 < ngrp) {  // the first tile's X into its (DMA-free) tile region now: xg dies here
+      float* tb0 = tl + half * TSZ;
+      const int r = htid >> 3, q = htid & 7;
+#pragma unroll
+      for (int i = 0; i < 10; i++) tb0[X + (q * 10 + i) * LDP + r] = xg[i];
+    }
   } else {
     stage_net<L1, NTHR>(A.params, w, net);
   }
@@ -708,8 +739,9 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     const float* wb = tl + zo;
     const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
     __syncthreads();  // the previous tile's LDS reads are done (and the weights staged)
-    if (!AK_GRAD1_PREFETCH || grp != grp0) loads(tile);
-    {
+    if (IMG && grp == grp0) gather_h(tile);  // X of the first tile is in LDS already (before the loop)
+    else {
+      if (!AK_GRAD1_PREFETCH || grp != grp0) loads(tile);
       const int r = htid >> 3, q = htid & 7;
 #pragma unroll
       for (int i = 0; i < 10; i++) tb[X + (q * 10 + i) * LDP + r] = xg[i];
@@ -892,8 +924,8 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     // items (into its tile region) and stores the combined gW2; half 0 hands over gW2 and stores
     // the combined gW1 and vector items
     __syncthreads();  // every tile read is done
-    float* xo = tl + WEND + half * TSZ;  // this half's hand-over region, [component][256]
-    const float* xi = tl + WEND + (1 - half) * TSZ;
+    float* xo = tl + TBASE + half * TSZ;  // this half's hand-over region, [component][256]
+    const float* xi = tl + TBASE + (1 - half) * TSZ;
     if (half == 1) {
 #pragma unroll
       for (int j = 0; j < 5; j++)

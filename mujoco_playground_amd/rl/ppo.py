@@ -304,7 +304,7 @@ class PPO:
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
         d.world = self.world
         d.log_std_min = float("-inf") if self.log_std_min is None else float(self.log_std_min)
-        self.set_weight_image(False, d)
+        self.set_weight_image(True, d)
         return d
 
     def set_epoch_buffers(self, on: bool, d=None):
@@ -316,12 +316,11 @@ class PPO:
                                          else (None, None))
 
     def set_weight_image(self, on: bool, d=None):
-        """on: the gradient launches copy each net's weights into LDS from a pre-laid-out image that
-        every Adam step keeps current (ackppo_train_desc weight_image; the same bits); off (default):
-        they transpose the parameter vector themselves. Measured (profiles/r04l_ppo_timing.log, the
-        two-tile gradient workgroups): 32.5 us per minibatch with the image against 32.1 without --
-        the gradient launch gains 0.4 us (21.07 -> 20.71), the Adam launch's scatter into the image
-        costs as much (4.99 -> 5.34)."""
+        """on (default): the gradient launches copy each net's weights into LDS from a pre-laid-out
+        image that every Adam step keeps current (ackppo_train_desc weight_image; the same bits), by
+        LDS-DMA, with the first tile's index and observation-row gathers in flight under the copies;
+        off: they load and transpose the parameter vector themselves, then gather. (Round 4, before the
+        gathers overlapped the copies: 32.5 us per minibatch with the image against 32.1 without.)"""
         d = self._desc if d is None else d
         d.weight_image = self.weight_image.data_ptr() if on else None
 
