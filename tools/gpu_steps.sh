@@ -9,6 +9,8 @@
 #   bench[=ARGS]       python bench.py ARGS (comma-separated flags, e.g. bench=--steps,20,--warmup,5)
 #   prof               rocprofv3 --kernel-trace --stats of the default bench command
 #   pmc                tools/profile_pmc.py (separate --pmc passes)
+#   py=SCRIPT,ARGS     python3 -u SCRIPT ARGS
+#   profpy=SCRIPT,ARGS rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS
 #   mfma               tools/profile_mfma.py
 #   kbench             tools/ppo_kbench.py
 #   quad=LIB:EPW,...   tools/probes/quad_time.py over step-library builds (diag_libs/*.so)
@@ -40,6 +42,11 @@ for step in "$@"; do
       (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o b -- python3 "$R/bench.py" --no-cpu > "$R/gpurun_out/${TAG}_prof.log" 2>&1) \
         || { echo "STEP_FAIL prof"; tail -20 "gpurun_out/${TAG}_prof.log"; exit 1; }
       find "gpurun_out/${TAG}_prof" -name "*kernel_stats.csv" | head -3 ;;
+    profpy)  # rocprofv3 kernel trace + stats of a python script: profpy=SCRIPT,ARGS...
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_profpy" -o p -- python3 "$R/"${val//,/ } > "$R/gpurun_out/${TAG}_profpy.log" 2>&1) \
+        || { echo "STEP_FAIL profpy"; tail -20 "gpurun_out/${TAG}_profpy.log"; exit 1; }
+      tail -3 "gpurun_out/${TAG}_profpy.log" ;;
+    py) run py 600 python3 -u ${val//,/ } ;;
     pmc) run pmc 900 python3 tools/profile_pmc.py ;;
     mfma) run mfma 600 python3 tools/profile_mfma.py ;;
     kbench) run kbench 600 python3 tools/ppo_kbench.py ${val//,/ } ;;

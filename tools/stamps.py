@@ -122,7 +122,8 @@ def main():
             if quad and k == 200:  # both waves' timeline from the dynamics wave's first stamp of the step
                 tl = [(1, "dyn: loaded"), (4, "dyn: contacts done"), (5, "dyn: Newton starts"),
                       (6, "dyn: Newton done"), (9, "dyn: at barrier 1"), (13, "dyn: past barrier 1"),
-                      (10, "dyn: stored"), (11, "obs: starts"), (12, "obs: at barrier 1")]
+                      (10, "dyn: stored"), (11, "obs: starts"), (14, "obs: slots published"), (12, "obs: at barrier 1"),
+                      (2, "dyn: dynamics entry"), (3, "dyn: M/bias/a0 done")]
                 print("  timeline (median cycles after dyn stamp 0): " + ", ".join(
                     f"{nm} {np.median(s[i] - s[0]):.0f}" for i, nm in tl if s[i].any()))
         d = np.median(np.concatenate(res, axis=1), axis=1)
