@@ -372,6 +372,8 @@ class PPO:
               progress_bar: bool = False):
         if reset_num_timesteps:
             self.num_timesteps = 0
+        else:  # stable-baselines3 semantics: a continued run learns total_timesteps more
+            total_timesteps += self.num_timesteps
         it = 0
         t0 = time.perf_counter()
         while self.num_timesteps < total_timesteps:

@@ -525,8 +525,10 @@ def test_ppo_data_parallel_two_ranks():
 
 def test_ppo_learns_the_variant_task():
     """The learner learns goal reaching on the opt-in learnable variant (action_repeat 10, nohit_clear;
-    include/ackphys.h): deterministic-policy success from fresh resets rises from 0 to >= 5 % within 100
-    PPO iterations (26 M env-steps; profiles/train/r03_variant_r10*.jsonl: 11 % at 100, 69 % at 1500).
+    include/ackphys.h): deterministic-policy success from fresh resets rises from 0 to >= 5 % within 200
+    PPO iterations (52 M env-steps; profiles/train/r03_variant_r10*.jsonl: 11 % at 100, 69 % at 1500).
+    At 100 iterations the number is seed noise (1-24 % over seeds 0-3 and 1-ulp solver changes,
+    tools/probes/variant_learn.py); at 200 every measured seed and build is >= 10 %.
     The reference task itself cannot be learned."""
     import os
     import sys
@@ -539,7 +541,7 @@ def test_ppo_learns_the_variant_task():
     model = PPO("MlpPolicy", venv, n_steps=64, batch_size=8192, n_epochs=10, seed=0)
     assert model.fused_rollout
     s0, _, _ = evaluate(model, horizon=1000, **kw)
-    model.learn(total_timesteps=100 * 64 * 4096)
+    model.learn(total_timesteps=200 * 64 * 4096)
     s1, steps, _ = evaluate(model, horizon=1000, **kw)
     print("success", s0, "->", s1, "steps to goal", steps)
     assert s0 == 0.0 and s1 >= 0.05
