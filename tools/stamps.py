@@ -99,7 +99,8 @@ def main():
             nt = allv[NSTAMP * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
                 print("  newton phases (median cycles/wave, summed over iterations): " + ", ".join(
-                    f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"])))
+                    f"{nm} {np.median(nt[i]):.0f}" for i, nm in enumerate(["grad+H", "chol+solve", "Jp+Mp", "LS", "update"]))
+                    + f"; sum {np.median(nt.sum(0)):.0f} vs newton span {np.median(s[6] - s[5]):.0f}")
             its = its[: 64 * nb]
             if quad:
                 its = its.reshape(nb, 64)[:, :epw].reshape(-1)
