@@ -19,14 +19,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 
 
-def child(lib, steps, scene, contacts):
+def child(lib, steps, scene, contacts, variant="auto"):
     sys.path.insert(0, REPO)
     import torch
     from mujoco_playground_amd import _lib
     _lib.LIB_PATH = os.path.abspath(lib)
     from mujoco_playground_amd.sim import BatchedAckermannSim
     dev = torch.device("cuda:0")
-    sim = BatchedAckermannSim(4096, dev, seed=0, contacts=contacts, scene=scene)
+    sim = BatchedAckermannSim(4096, dev, seed=0, contacts=contacts, scene=scene, variant=variant)
     sim.reset()
     acts = sim.random_actions(200 + 3 * steps, seed=0)
     sim.rollout(acts[:200], want_info=False, per_step_outputs=False)
@@ -52,10 +52,11 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--scene", default="flat", help="flat, obstacles or both")
     ap.add_argument("--contacts", type=int, default=1)
+    ap.add_argument("--variant", default="auto")
     ap.add_argument("--child", default=None)
     a = ap.parse_args()
     if a.child:
-        child(a.child, a.steps, a.scene, bool(a.contacts))
+        child(a.child, a.steps, a.scene, bool(a.contacts), a.variant)
         return
     rc = 0
     for spec in a.libs:
@@ -65,7 +66,7 @@ def main():
             env["ACKPHYS_QUAD_EPW"] = epw
         for scene in (("flat", "obstacles") if a.scene == "both" else (a.scene,)):
             r = subprocess.run([sys.executable, __file__, "--child", lib, "--steps", str(a.steps), "--scene", scene,
-                                "--contacts", str(a.contacts)], env=env, timeout=300)
+                                "--contacts", str(a.contacts), "--variant", a.variant], env=env, timeout=300)
             if r.returncode:
                 print(f"{spec}: exit {r.returncode}", flush=True)
                 sys.exit(r.returncode)
