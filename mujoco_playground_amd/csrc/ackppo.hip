@@ -74,10 +74,25 @@ using ppm::gauss_term;
 using ppm::f4v;   // f32 MFMA 16x16x4 (exact f32 products, a k-ordered fmaf chain; ackppo_math.inc)
 using ppm::mfma4;
 
+// Sum over the wave, the same rounded value in every lane. Symmetric pairings only (every step adds
+// a lane's value and its partner's, so both end with the same bits): xor 1 and xor 2 inside quads,
+// the 8-lane and 16-lane mirrors (DPP row_half_mirror / row_mirror), then row pairs and wave halves
+// by permlane16 / permlane32 swaps. (As xor shuffles each step was a ds_bpermute round trip through
+// LDS, ~120 cycles: the gradient launch's four loss sums took ~3.4k cycles at the end of every
+// workgroup.) Every lane of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x141>(v);  // row_half_mirror: lane i <-> 7 - i of each 8
+  v += dpp_f<0x140>(v);  // row_mirror: lane i <-> 15 - i of each 16
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // (even row, odd row) in every lane
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // (low half, high half) in every lane
 }
 // LDS written by some lanes of this wave, read by others: order the accesses (one wave's LDS
 // operations execute in order) and keep the compiler from moving them across
@@ -924,6 +939,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     // items (into its tile region) and stores the combined gW2; half 0 hands over gW2 and stores
     // the combined gW1 and vector items
     __syncthreads();  // every tile read is done
+    PSTAMP(9);
     float* xo = tl + TBASE + half * TSZ;  // this half's hand-over region, [component][256]
     const float* xi = tl + TBASE + (1 - half) * TSZ;
     if (half == 1) {
@@ -940,6 +956,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
         for (int r = 0; r < 4; r++) xo[(4 * j + r) * GRAD_THREADS + htid] = gw2[j][r];
     }
     __syncthreads();
+    PSTAMP(10);
     if (half == 0) {
 #pragma unroll
       for (int j = 0; j < 5; j++)
@@ -978,6 +995,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       for (int j = 0; j < 4; j++) g[ow2 + u * H + 16 * j + li] = gw2[j][r];
     }
   }
+  PSTAMP(11);
   // loss sums: per wave, then the four waves in order through LDS (the tile is done)
   la = wave_sum(la);
   lb = wave_sum(lb);
@@ -991,6 +1009,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     tl[X + 4 * wave8 + 3] = ln;
   }
   __syncthreads();
+  PSTAMP(12);
   if (tid < 4) {
     float s = (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]);
     if constexpr (NT == 2) s = s + ((tl[X + 16 + tid] + tl[X + 20 + tid]) + (tl[X + 24 + tid] + tl[X + 28 + tid]));
