@@ -84,15 +84,22 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+// v + (v of lane ^ 16) and v + (v of lane ^ 32), as the xor-shuffle sums give them bit for bit (one
+// swap and one add; the add is commutative, so the odd row's lanes round the same sum)
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
   v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
   v += dpp_f<0x141>(v);  // row_half_mirror: lane i <-> 7 - i of each 8
   v += dpp_f<0x140>(v);  // row_mirror: lane i <-> 15 - i of each 16
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // (even row, odd row) in every lane
-  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // (low half, high half) in every lane
+  return sum_xor32(sum_xor16(v));  // row pairs, then the wave halves
 }
 // LDS written by some lanes of this wave, read by others: order the accesses (one wave's LDS
 // operations execute in order) and keep the compiler from moving them across
@@ -812,10 +819,9 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
         const int k = 16 * q + ((j + 2 * q) & 15);
         m = fmaf(wb[HW + d * H + k], tb[H2 + k * LDP + hs], m);
       }
-      m += __shfl_xor(m, 16, 64);
-      m += __shfl_xor(m, 32, 64);
+      m = sum_xor32(sum_xor16(m));  // = m + m^16, then + ^32 (the xor-shuffle sums, bit for bit)
       m += wb[HB + d];
-      const float mo = __shfl_xor(m, 8, 64);  // the other dimension's mean
+      const float mo = dpp_f<0x128>(m);  // the other dimension's mean: lane ^ 8 (row_ror 8)
       const float mu0 = d ? mo : m, mu1 = d ? m : mo;
       const float ls0 = wb[HB + 2], ls1 = wb[HB + 3];
       const float logp = gauss_term(hin[0], mu0, ls0) + gauss_term(hin[1], mu1, ls1);
@@ -848,9 +854,8 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
         const int k = 8 * q + ((j + 2 * q) & 7);
         v = fmaf(wb[HW + k], tb[H2 + k * LDP + hs], v);
       }
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+      v += dpp_f<0x128>(v);         // + lane ^ 8 (row_ror 8)
+      v = sum_xor32(sum_xor16(v));  // + ^16, + ^32
       v += wb[HB];
       if (q == 0) {
         const float R = hin[0];
