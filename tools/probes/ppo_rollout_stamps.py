@@ -18,7 +18,7 @@ NSTAMP = 24
 
 def main(scene):
     from mujoco_playground_amd import _lib
-    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libackphys_stamps.so")  # before the first load
+    _lib.LIB_PATH = os.path.join(ROOT, "diag_libs", "libackphys_stamps.so")  # tools/build_diag.sh; before the first load
     import torch
     from mujoco_playground_amd.rl import AckermannVecEnv
     from mujoco_playground_amd.rl.ppo import PPO
