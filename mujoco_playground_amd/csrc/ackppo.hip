@@ -772,18 +772,39 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     PSTAMP(1);
     {  // layer 1: H1 [64 x 32] = tanh(W1 X + b1)
       f4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      // software-pipelined by blocks of KB k-steps: block b + 1's operand reads are issued before
+      // block b's MFMAs, so the LDS latency hides under them (left to the scheduler, each k-step
+      // read its X pair into the same two registers and waited for it)
+      constexpr int KB = 5, NBK = 20 / KB;
+      float bias[4];  // read with the first operands (the epilogue waited for each in turn)
 #pragma unroll
-      for (int k0 = 0; k0 < 80; k0 += 4) {
-        const int k = k0 + lk;
-        const float wa = wb[w1t(k, ub + li)];
-        a0 = mfma4(wa, tb[X + k * LDP + li], a0);
-        a1 = mfma4(wa, tb[X + k * LDP + 16 + li], a1);
+      for (int r = 0; r < 4; r++) bias[r] = wb[B1 + ub + 4 * lk + r];
+      float wa[2][KB], xa[2][KB], xb[2][KB];
+      auto ld1 = [&](int b, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < KB; s++) {
+          const int k = 4 * (b * KB + s) + lk;
+          wa[buf][s] = wb[w1t(k, ub + li)];
+          xa[buf][s] = tb[X + k * LDP + li];
+          xb[buf][s] = tb[X + k * LDP + 16 + li];
+        }
+      };
+      ld1(0, 0);
+#pragma unroll
+      for (int b = 0; b < NBK; b++) {
+        if (b + 1 < NBK) ld1(b + 1, (b + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < KB; s++) {
+          a0 = mfma4(wa[b & 1][s], xa[b & 1][s], a0);
+          a1 = mfma4(wa[b & 1][s], xb[b & 1][s], a1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int u = ub + 4 * lk + r;
-        const float bb = wb[B1 + u];
+        const float bb = bias[r];
         tb[H1 + u * LDP + li] = ftanh(a0[r] + bb);
         tb[H1 + u * LDP + 16 + li] = ftanh(a1[r] + bb);
       }
@@ -792,18 +813,36 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     PSTAMP(2);
     {  // layer 2: H2 [64 x 32] = tanh(W2 H1 + b2)
       f4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      constexpr int KB = 4, NBK = H / 4 / KB;  // pipelined as layer 1
+      float bias[4];
 #pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;
-        const float wa = wb[w2(ub + li, k)];
-        a0 = mfma4(wa, tb[H1 + k * LDP + li], a0);
-        a1 = mfma4(wa, tb[H1 + k * LDP + 16 + li], a1);
+      for (int r = 0; r < 4; r++) bias[r] = wb[B2 + ub + 4 * lk + r];
+      float wa[2][KB], xa[2][KB], xb[2][KB];
+      auto ld2 = [&](int b, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < KB; s++) {
+          const int k = 4 * (b * KB + s) + lk;
+          wa[buf][s] = wb[w2(ub + li, k)];
+          xa[buf][s] = tb[H1 + k * LDP + li];
+          xb[buf][s] = tb[H1 + k * LDP + 16 + li];
+        }
+      };
+      ld2(0, 0);
+#pragma unroll
+      for (int b = 0; b < NBK; b++) {
+        if (b + 1 < NBK) ld2(b + 1, (b + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < KB; s++) {
+          a0 = mfma4(wa[b & 1][s], xa[b & 1][s], a0);
+          a1 = mfma4(wa[b & 1][s], xb[b & 1][s], a1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int u = ub + 4 * lk + r;
-        const float bb = wb[B2 + u];
+        const float bb = bias[r];
         tb[H2 + u * LDP + li] = ftanh(a0[r] + bb);
         tb[H2 + u * LDP + 16 + li] = ftanh(a1[r] + bb);
       }
