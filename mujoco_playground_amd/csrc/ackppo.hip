@@ -927,12 +927,30 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     PSTAMP(5);
     f4v d1a = {0.f, 0.f, 0.f, 0.f}, d1b = {0.f, 0.f, 0.f, 0.f};
     {  // W2^T D2 for the wave's layer-1 units, and gW2 [64 x 64] += D2 H1^T (rows = the wave's units)
+      {  // pipelined as the forward layers
+        constexpr int KB = 4, NBK = H / 4 / KB;
+        float wt[2][KB], da[2][KB], db[2][KB];
+        auto ldb = [&](int b, int buf) __attribute__((always_inline)) {
 #pragma unroll
-      for (int k0 = 0; k0 < H; k0 += 4) {
-        const int k = k0 + lk;  // layer-2 unit
-        const float wt = wb[w2(k, ub + li)];
-        d1a = mfma4(wt, tb[D2 + k * LDP + li], d1a);
-        d1b = mfma4(wt, tb[D2 + k * LDP + 16 + li], d1b);
+          for (int s = 0; s < KB; s++) {
+            const int k = 4 * (b * KB + s) + lk;  // layer-2 unit
+            wt[buf][s] = wb[w2(k, ub + li)];
+            da[buf][s] = tb[D2 + k * LDP + li];
+            db[buf][s] = tb[D2 + k * LDP + 16 + li];
+          }
+        };
+        ldb(0, 0);
+#pragma unroll
+        for (int b = 0; b < NBK; b++) {
+          if (b + 1 < NBK) ldb(b + 1, (b + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 0; s < KB; s++) {
+            d1a = mfma4(wt[b & 1][s], da[b & 1][s], d1a);
+            d1b = mfma4(wt[b & 1][s], db[b & 1][s], d1b);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);  // scheduling regions: bounded register pressure
 #pragma unroll
