@@ -654,6 +654,21 @@ __device__ __forceinline__ int vec_offset_g1(int net, int i) {
   return i < 192 ? ACKPPO_OFF_VAL_W + (i - 128) : ACKPPO_OFF_VAL_B;
 }
 
+// the workgroup's loss sums into its loss row (threads 0-3: sum tid of the four)
+__device__ __forceinline__ void loss_row(const GradArgs& A, int row, int net, float s) {
+  const int tid = threadIdx.x;
+  float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
+  if (net == 0) {
+    lp[tid == 0 ? 0 : tid + 1] = s;  // policy loss, clipped count, approx-kl sum, samples
+    if (tid == 0) lp[5] = lp[6] = lp[7] = 0.0f;
+  } else if (tid == 0) {
+    lp[1] = s;  // value loss sum
+  }
+}
+namespace g1 {
+constexpr int LS_SLOT = 22 * GRAD_THREADS;  // a half's four waves' loss sums, after its hand-over words
+static_assert(LS_SLOT + 16 <= TSZ, "loss sums in the hand-over region");
+}  // namespace g1
 template <bool IMG = false>
 __device__ __forceinline__ void grad1(const GradArgs& A) {
   using namespace g1;
@@ -697,37 +712,40 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       xg[i] = (r < nvalid && k < NOBS) ? v : 0.0f;
     }
   };
-  auto gather_h = [&](int tile) __attribute__((always_inline)) {
+  // the heads' per-sample inputs, unmasked (a clamped sample past the batch reads valid rows): the
+  // heads zero them for invalid samples where they use them, so nothing waits for these loads
+  // before then (selects right behind the loads had each wave wait out the index and the row
+  // latencies before layer 1)
+  auto head_idx = [&](int tile) __attribute__((always_inline)) {
     const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
-    const int sidx = A.idx[nvalid > 0 ? s0 + min(hs, nvalid - 1) : 0];
-    const bool hv = hs < nvalid;
-    if (net == 0) {
-      const float2 a = *reinterpret_cast<const float2*>(A.actions + 2 * (size_t)sidx);
-      const float o = A.old_logp[sidx], ad = A.adv[sidx];
-      hin[0] = hv ? a.x : 0.0f;
-      hin[1] = hv ? a.y : 0.0f;
-      hin[2] = hv ? o : 0.0f;
-      hin[3] = hv ? ad : 0.0f;
-    } else {
-      const float rt = A.ret[sidx];
-      hin[0] = hv ? rt : 0.0f;
-    }
+    return A.idx[nvalid > 0 ? s0 + min(hs, nvalid - 1) : 0];
+  };
+  // (straight-line: the critic loads the actor's three words too and never reads them -- with a
+  // branch per net the two paths' registers were merged by copies that waited for the loads)
+  auto gather_h = [&](int sidx) __attribute__((always_inline)) {
+    hin[0] = *(net ? A.ret + sidx : A.actions + 2 * (size_t)sidx);
+    hin[1] = A.actions[2 * (size_t)sidx + 1];
+    hin[2] = A.old_logp[sidx];
+    hin[3] = A.adv[sidx];
   };
   auto loads = [&](int tile) __attribute__((always_inline)) {
     gather_x(tile, row_idx(tile));
-    gather_h(tile);
   };
 
   // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
   // overlaps it; the registers they hold through the staging cost a few spill slots)
   if (AK_GRAD1_PREFETCH && !IMG && grp0 < ngrp) loads(NT * grp0 + half);
+  int hx = 0;  // grad1i: the first tile's heads sample index (loaded with the rows' index)
   if constexpr (IMG) {
     // the first tile's sample indices, then the weight image's LDS-DMA copies (no registers), then the
     // rows those indices address: the two dependent gathers run under the copies instead of after them
     // (vmcnt retires in issue order, so the gathers' addresses wait only for the older index loads)
     // (the heads' inputs are gathered in the loop: they are needed only after both layers)
     int ir = 0;
-    if (grp0 < ngrp) ir = row_idx(NT * grp0 + half);
+    if (grp0 < ngrp) {
+      ir = row_idx(NT * grp0 + half);
+      hx = head_idx(NT * grp0 + half);
+    }
     stage_image<NTHR>(A.wimg + net * WIMG, w);
     if (grp0 < ngrp) gather_x(NT * grp0 + half, ir);
     // the LDS-DMA copies count in vmcnt, not lgkmcnt: drain them before the first barrier makes the
@@ -761,13 +779,15 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     const float* wb = tl + zo;
     const int s0 = tile * T, nvalid = max(0, min(T, A.batch - s0));
     __syncthreads();  // the previous tile's LDS reads are done (and the weights staged)
-    if (IMG && grp == grp0) gather_h(tile);  // X of the first tile is in LDS already (before the loop)
-    else {
+    int sidx = hx;  // grad1i's first tile: X in LDS already, the heads' index loaded with the rows'
+    if (!(IMG && grp == grp0)) {
       if (!AK_GRAD1_PREFETCH || grp != grp0) loads(tile);
       const int r = htid >> 3, q = htid & 7;
 #pragma unroll
       for (int i = 0; i < 10; i++) tb[X + (q * 10 + i) * LDP + r] = xg[i];
+      sidx = head_idx(tile);
     }
+    gather_h(sidx);  // one load site: hin stays in flight through both layers
     __syncthreads();
     PSTAMP(1);
     {  // layer 1: H1 [64 x 32] = tanh(W1 X + b1)
@@ -850,6 +870,8 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     __syncthreads();
     PSTAMP(3);
     const bool hvalid = hs < nvalid;
+#pragma unroll
+    for (int i = 0; i < 4; i++) hin[i] = hvalid ? hin[i] : 0.0f;
     if (net == 0) {  // actor heads: mu[d] of sample hs, a 16-term quarter per lane, butterflies over q
       const int d = (lane >> 3) & 1, q = lane >> 4;
       float m = 0.0f;
@@ -996,6 +1018,12 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   float* g = A.gpart + (size_t)row * P;
   const int ow1 = net ? ACKPPO_OFF_VF_W1 : ACKPPO_OFF_PI_W1, ow2 = net ? ACKPPO_OFF_VF_W2 : ACKPPO_OFF_PI_W2;
   bool st_w1 = true, st_w2 = true;
+  // loss sums: per wave here, then the waves in order through LDS (with NT == 2, behind the
+  // hand-over's two barriers: a barrier after the partial-row stores waited for those stores)
+  la = wave_sum(la);
+  lb = wave_sum(lb);
+  lc = wave_sum(lc);
+  ln = wave_sum(ln);
   if constexpr (NT == 2) {
     // the halves' sums combined through LDS, tile 2 g's first: half 1 hands over gW1 and the vector
     // items (into its tile region) and stores the combined gW2; half 0 hands over gW2 and stores
@@ -1004,6 +1032,13 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     PSTAMP(9);
     float* xo = tl + TBASE + half * TSZ;  // this half's hand-over region, [component][256]
     const float* xi = tl + TBASE + (1 - half) * TSZ;
+    if (lane == 0) {
+      float* ls = xo + LS_SLOT + 4 * wave;
+      ls[0] = la;
+      ls[1] = lb;
+      ls[2] = lc;
+      ls[3] = ln;
+    }
     if (half == 1) {
 #pragma unroll
       for (int j = 0; j < 5; j++)
@@ -1035,6 +1070,14 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       st_w1 = false;
     }
   }
+  if constexpr (NT == 2) {
+    if (tid < 4) {
+      const float* ls = tl + TBASE + LS_SLOT;
+      const float s = ((ls[tid] + ls[4 + tid]) + (ls[8 + tid] + ls[12 + tid])) +
+                      ((ls[TSZ + tid] + ls[TSZ + 4 + tid]) + (ls[TSZ + 8 + tid] + ls[TSZ + 12 + tid]));
+      loss_row(A, row, net, s);
+    }
+  }
   if (st_w1) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -1058,30 +1101,17 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     }
   }
   PSTAMP(11);
-  // loss sums: per wave, then the four waves in order through LDS (the tile is done)
-  la = wave_sum(la);
-  lb = wave_sum(lb);
-  lc = wave_sum(lc);
-  ln = wave_sum(ln);
-  __syncthreads();
-  if (lane == 0) {
-    tl[X + 4 * wave8 + 0] = la;
-    tl[X + 4 * wave8 + 1] = lb;
-    tl[X + 4 * wave8 + 2] = lc;
-    tl[X + 4 * wave8 + 3] = ln;
-  }
-  __syncthreads();
-  PSTAMP(12);
-  if (tid < 4) {
-    float s = (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]);
-    if constexpr (NT == 2) s = s + ((tl[X + 16 + tid] + tl[X + 20 + tid]) + (tl[X + 24 + tid] + tl[X + 28 + tid]));
-    float* lp = A.lpart + (size_t)row * ACKPPO_NLOSS;
-    if (net == 0) {
-      lp[tid == 0 ? 0 : tid + 1] = s;  // policy loss, clipped count, approx-kl sum, samples
-      if (tid == 0) lp[5] = lp[6] = lp[7] = 0.0f;
-    } else if (tid == 0) {
-      lp[1] = s;  // value loss sum
+  if constexpr (NT == 1) {
+    __syncthreads();  // the tile is done
+    if (lane == 0) {
+      tl[X + 4 * wave8 + 0] = la;
+      tl[X + 4 * wave8 + 1] = lb;
+      tl[X + 4 * wave8 + 2] = lc;
+      tl[X + 4 * wave8 + 3] = ln;
     }
+    __syncthreads();
+    PSTAMP(12);
+    if (tid < 4) loss_row(A, row, net, (tl[X + tid] + tl[X + 4 + tid]) + (tl[X + 8 + tid] + tl[X + 12 + tid]));
   }
   PSTAMP(15);
   PRSTAMP(14);
