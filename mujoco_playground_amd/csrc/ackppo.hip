@@ -690,6 +690,9 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
   // heads' lane roles: wave w, samples 8 w + (lane & 7); actor lanes (d = (lane >> 3) & 1, quarter
   // q = lane >> 4 of the 64 inputs), critic lanes (eighth q = lane >> 3)
   const int hs = 8 * wave + (lane & 7);
+  // the minibatch's advantage moments, read first (the actor heads read them in the loop, where the
+  // load sat on the heads phase's critical path)
+  const float adv_mean = A.stats[0], adv_inv_sd = A.stats[1];
   float xg[10];
   float hin[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   // a tile's gathers: the observation rows (X) and the heads' per-sample inputs (hin), each behind its
@@ -888,7 +891,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
       const float logp = gauss_term(hin[0], mu0, ls0) + gauss_term(hin[1], mu1, ls1);
       const float lr = logp - hin[2];
       const float r = fexp(lr);
-      const float adv = (hin[3] - A.stats[0]) * A.stats[1];
+      const float adv = (hin[3] - adv_mean) * adv_inv_sd;
       const float rc = fminf(fmaxf(r, 1.0f - A.clip), 1.0f + A.clip);
       const float l1 = adv * r, l2 = adv * rc;
       // d(-min(l1, l2))/dlogp: through l1 when it is the minimum (ties: torch.min splits the
@@ -1614,35 +1617,42 @@ __device__ __forceinline__ void adam_block_update(const UpdArgs& A, int b, float
 // ackppo_reduce1_kernel) into grad, the loss rows on workgroup 0, and S_b
 constexpr int RA_G = 8;
 constexpr int RA_THREADS = RA_G * NB_P;
+// RKV: the row slots a thread loads (RK = GRAD_MAX_BLOCKS / RA_G in general; RK / 2 when nblk <= 128, the
+// bench's 8192-sample minibatch). Every load is issued unconditionally from a clamped row and column
+// and masked after (guarded loads were one exec-mask branch each); with RKV < RK the slots past RKV
+// are the zeros the RK form adds to acc[0], so one + 0.0f stands for them (a -0.0 sum becomes +0.0
+// there too): the same bits either way.
+template <int RKV>
 __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P + 1], float* lred) {
   const int tid = threadIdx.x, b = blockIdx.x;
   const int pidx = b * NB_P + tid;  // threads 0-127: the parameter this thread finishes
   const bool own = tid < NB_P && pidx < P;
   constexpr int RK = GRAD_MAX_BLOCKS / RA_G;
-  static_assert(RK % 4 == 0, "row blocks of four");
+  static_assert(RK % 4 == 0 && RKV % 4 == 0 && RKV <= RK, "row blocks of four");
   static_assert(P % 4 == 0 && NB_P % 4 == 0, "whole 16-B vectors per row and block");
   {
-    const int pl = tid & (NB_P - 1), g = tid / NB_P;
+    const int pl = tid & (NB_P - 1), g = __builtin_amdgcn_readfirstlane(tid / NB_P);  // g: wave-uniform
     const int pcol = b * NB_P + pl;
-    float x[RK];
+    const float* col = A.gpart + min(pcol, P - 1);
+    float x[RKV];
 #pragma unroll
-    for (int k = 0; k < RK; k++) {
-      const int r = g + k * RA_G;
-      x[k] = (pcol < P && r < A.nblk) ? A.gpart[(size_t)r * P + pcol] : 0.0f;
-    }
+    for (int k = 0; k < RKV; k++) x[k] = col[(size_t)min(g + k * RA_G, A.nblk - 1) * P];
+#pragma unroll
+    for (int k = 0; k < RKV; k++) x[k] = (pcol < P && g + k * RA_G < A.nblk) ? x[k] : 0.0f;
     int nmain = 0;
 #pragma unroll
     for (int j = 0; j < RK / 4; j++) nmain += (g + 4 * RA_G * j + 3 * RA_G < A.nblk) ? 1 : 0;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < RK / 4; j++)
+    for (int j = 0; j < RKV / 4; j++)
       if (j < nmain) {
 #pragma unroll
         for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
       }
 #pragma unroll
-    for (int k = 0; k < RK; k++)
+    for (int k = 0; k < RKV; k++)
       if (k >= 4 * nmain) acc[0] += x[k];
+    if constexpr (RKV < RK) acc[0] += 0.0f;
     red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
   __syncthreads();
@@ -1670,15 +1680,29 @@ __device__ __forceinline__ float reduce_rows(const UpdArgs& A, float (*red)[NB_P
   }
   return gv;
 }
-extern "C" __global__ void __launch_bounds__(RA_THREADS) ackppo_reduce_norm_kernel(UpdArgs A) {
+template <int RKV>
+__device__ __forceinline__ void reduce_norm(const UpdArgs& A) {
   __shared__ float red[RA_G][NB_P + 1];
   __shared__ float lred[256];
   __shared__ float nred[2];
   const int tid = threadIdx.x, b = blockIdx.x;
-  const float gv = reduce_rows(A, red, lred);
+  const float gv = reduce_rows<RKV>(A, red, lred);
   if (!A.sq) return;
   const float sb = norm_block_sq(gv, A.scale, b, nred);  // every row read above is done (barriers)
   if (tid == 0) A.gpart[(size_t)b * NB_P] = sb;
+}
+extern "C" __global__ void __launch_bounds__(RA_THREADS) ackppo_reduce_norm_kernel(UpdArgs A) {
+  reduce_norm<GRAD_MAX_BLOCKS / RA_G>(A);
+}
+extern "C" __global__ void __launch_bounds__(RA_THREADS) ackppo_reduce_norm128_kernel(UpdArgs A) {  // nblk <= 128
+  reduce_norm<GRAD_MAX_BLOCKS / RA_G / 2>(A);
+}
+// the reduction launch for U.nblk partial rows
+void reduce_norm_launch(const UpdArgs& U, hipStream_t st) {
+  if (U.nblk <= GRAD_MAX_BLOCKS / 2)
+    hipLaunchKernelGGL(ackppo_reduce_norm128_kernel, dim3(NB_N), dim3(RA_THREADS), 0, st, U);
+  else
+    hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(RA_THREADS), 0, st, U);
 }
 // S_b of the gradient as it is now (the data-parallel path: after its all-reduce)
 extern "C" __global__ void __launch_bounds__(NB_P) ackppo_norm_blocks_kernel(UpdArgs A) {
@@ -1943,7 +1967,7 @@ void adam_scalars(double lr, double beta1, double beta2, double t, float& step_s
 // the norm from the reduction's block sums
 int reduce_adam_launch(UpdArgs& U, void* stream) {
   U.sq = 1;
-  hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(RA_THREADS), 0, (hipStream_t)stream, U);
+  reduce_norm_launch(U, (hipStream_t)stream);
   if (const int rc = launched("ackppo_reduce_norm")) return rc;
   hipLaunchKernelGGL(ackppo_adam_blocked_kernel, dim3(NB_N), dim3(256), 0, (hipStream_t)stream, U);
   return launched("ackppo_adam_blocked");
@@ -2072,7 +2096,7 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
         if ((rc = reduce_adam_launch(U, stream))) return rc;
       } else {
         U.sq = 0;
-        hipLaunchKernelGGL(ackppo_reduce_norm_kernel, dim3(NB_N), dim3(RA_THREADS), 0, st, U);
+        reduce_norm_launch(U, st);
         if ((rc = launched("ackppo_train: reduction"))) return rc;
         if ((rc = coll(d->grad, ACKPPO_NPARAM, ACKPPO_F32, "gradient"))) return rc;
         hipLaunchKernelGGL(ackppo_norm_blocks_kernel, dim3(NB_N), dim3(NB_P), 0, st, U);
