@@ -41,14 +41,17 @@ def main(scene):
         s = stamps.cpu().numpy()[: NSTAMP * nb].reshape(NSTAMP, nb).astype(np.int64)
         ok = (s[0] > 0) & (s[9] > 0) & (s[11] > 0) & (s[15] > 0) & (s[14] > 0)
         ok &= (s[16] > 0) & (s[17] > 0) & (s[18] > 0) & (s[19] > 0)
-        rows.append(np.stack([s[9] - s[0], s[12] - s[11], s[13] - s[12], s[14] - s[13], s[15] - s[14], s[15] - s[9],
-                              s[11] - s[0], s[15] - s[11], s[16] - s[13], s[17] - s[16], s[18] - s[17], s[19] - s[18],
-                              s[14] - s[19]])[:, ok])
+        # slot 13 is written by both waves (the observation wave's "bootstrap done", then the dynamics
+        # wave's "past barrier 1", which lands last): the bootstrap and policy spans are taken from
+        # stamps 12 and 14 together, and slot 13 is read as the dynamics wave's
+        rows.append(np.stack([s[9] - s[0], s[12] - s[11], s[14] - s[12], s[15] - s[14], s[13] - s[9],
+                              s[11] - s[0], s[15] - s[11], s[17] - s[16], s[18] - s[17], s[19] - s[18],
+                              s[14] - s[19], s[1] - s[0]])[:, ok])
     r = np.concatenate(rows, axis=1)
-    names = ["dyn: loaded -> barrier 1", "obs: observation", "obs: bootstrap", "obs: policy",
-             "obs: waits at barrier 1", "dyn: waits at barrier 1", "obs entry - dyn entry", "obs: entry -> past barrier 1",
-             "policy: layer 1 (+ head rows)", "policy: layer 2", "policy: heads", "policy: rollout rows",
-             "policy: sample + controller"]
+    names = ["dyn: loaded -> barrier 1", "obs: observation", "obs: bootstrap + policy", "obs: waits at barrier 1",
+             "dyn: at barrier 1 -> past it", "obs entry - dyn entry", "obs: entry -> past barrier 1",
+             "policy: layer 2", "policy: heads", "policy: rollout rows", "policy: sample + controller",
+             "dyn: loaded -> controller"]
     print(f"== {scene} scene, PPO rollout step T-2, {r.shape[1]} workgroup samples; cycles (median / p90)")
     for nm, v in zip(names, r):
         print(f"  {nm:30s} {np.median(v):9.0f} {np.percentile(v, 90):9.0f}")
