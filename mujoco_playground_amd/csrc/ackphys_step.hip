@@ -57,6 +57,19 @@ struct StampScope {
   }
 };
 #define STAMP_SCOPE StampScope _stamp_scope;
+// loop-top clocks of the multi-step kernels (tools/probes/step_clock.py): rows AK_NSTAMP + 69 .. 72 hold
+// the shader clock and the 100 MHz real-time counter at the loop top of the first and the last step
+// (thread 0 of each workgroup)
+#define LOOP_CLOCK(k, last)                                                                              \
+  do {                                                                                                   \
+    if (((k) == 0 || (k) == (last)) && threadIdx.x == 0) {                                               \
+      unsigned long long _c, _r;                                                                         \
+      asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(_c), "=s"(_r)::"memory"); \
+      const size_t _o = (k) == 0 ? 0 : 2;                                                                \
+      g_stamps[(AK_NSTAMP + 69 + _o) * (size_t)gridDim.x + blockIdx.x] = _c;                             \
+      g_stamps[(AK_NSTAMP + 70 + _o) * (size_t)gridDim.x + blockIdx.x] = _r;                             \
+    }                                                                                                    \
+  } while (0)
 // per-step roles of a multi-step kernel: flushed unless Args::stamp_skip (the PPO rollout keeps one step's)
 #define STAMP_SCOPE_A(A) StampScope _stamp_scope(!(A).stamp_skip);
 // Newton-phase accumulators (diag build): NT_MARK(ph) adds the cycles since the previous mark to phase ph
@@ -88,6 +101,9 @@ struct StampScope {
 #define NT_FLUSH
 #define STAMP_SCOPE
 #define STAMP_SCOPE_A(A)
+#define LOOP_CLOCK(k, last) \
+  do {                      \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
