@@ -171,17 +171,17 @@ def time_dp_update(model, device, stream, iters, train_ms, n_epochs, nmb):
     """The world > 1 update path timed on one GPU: ackppo_train's data-parallel sequence (every epoch's
     shuffle and advantage moments at the start of the call with 2 f64 all-reduces, then per minibatch
     the reduction, one 75 KB f32 all-reduce, the norm blocks and Adam) over a one-rank communicator,
-    on the same rollout buffer (untimed first call). "torch" = the default at world > 1: RCCL calls on
-    the communicator of torch's own ProcessGroupNCCL (a one-rank nccl process group here); "rccl" =
-    libackppo's own communicator (opt-in)."""
+    on the same rollout buffer (untimed first call). "rccl" = the default at world > 1: libackppo's own
+    communicator; "torch" = RCCL calls on the communicator of torch's own ProcessGroupNCCL (a one-rank
+    nccl process group here; opt-in until it has run on a multi-GPU node)."""
     import torch.distributed as dist
     out = {}
     made_pg = False
     if not dist.is_initialized():
-        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=device)
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)  # as shard.init: lazy comm
         made_pg = True
     try:
-        for kind in ("torch", "rccl"):
+        for kind in ("rccl", "torch"):
             model.set_collective(kind)
             model.train()
             ed = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -198,8 +198,9 @@ def time_dp_update(model, device, stream, iters, train_ms, n_epochs, nmb):
     finally:
         if made_pg:
             dist.destroy_process_group()
-    d = dict(out["torch"])
-    d.update({"collective": "torch (the default at world > 1)", "native_communicator": out["rccl"],
+    d = dict(out["rccl"])
+    d.update({"collective": "rccl (libackppo's own communicator, the default at world > 1)",
+              "torch_communicator": out["torch"],
               "collectives_per_iteration": n_epochs * nmb + 2, "bytes_per_minibatch_allreduce": 4 * 18764,
               "note": "ackppo_train with the RCCL hook on a one-rank communicator: the data-parallel sequence "
                       "every rank of configs[3] runs, each collective enqueued from C (no per-minibatch host "

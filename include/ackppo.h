@@ -196,7 +196,8 @@ typedef struct {
   float* exp_avg_sq;
   int32_t* perm;            /* [n_idx] */
   float* stats;             /* [nmb][2] */
-  double* moments;          /* with a hook: [3][nmb] float64, or [3][n_epochs][nmb] with perm_epochs / stats_epochs */
+  double* moments;          /* with a hook: [3][nmb] float64, or [3][n_epochs][nmb] with perm_epochs / stats_epochs
+                             * (its size in moments_count, the last field) */
   float* grad_partial;      /* [ackppo_grad_blocks(batch)][NPARAM], pad words zero */
   float* loss_partial;      /* [ackppo_grad_blocks(batch)][8] */
   float* grad;              /* [NPARAM] */
@@ -224,6 +225,9 @@ typedef struct {
    * n_epochs x nmb f64, one finalize launch -- 2 collectives per call instead of 2 per epoch */
   int32_t* perm_epochs;
   float* stats_epochs;
+  /* float64 elements available at `moments` (required with a hook): at least 3 * nmb, or
+   * 3 * n_epochs * nmb with perm_epochs / stats_epochs; a smaller buffer is refused (EINVAL) */
+  int64_t moments_count;
 } ackppo_train_desc;
 
 /* SB3 PPO.train (ppo.py:196-279 of SB3 2.7.0) on the device: for each epoch, the minibatch

@@ -83,7 +83,8 @@ class TrainDesc(C.Structure):
                 ("loss_partial", C.c_void_p), ("grad", C.c_void_p), ("loss_acc", C.c_void_p),
                 ("grad_norm_out", C.c_void_p), ("world", C.c_int), ("allreduce", C.c_void_p),
                 ("allreduce_user", C.c_void_p), ("log_std_min", C.c_float),
-                ("weight_image", C.c_void_p), ("perm_epochs", C.c_void_p), ("stats_epochs", C.c_void_p)]
+                ("weight_image", C.c_void_p), ("perm_epochs", C.c_void_p), ("stats_epochs", C.c_void_p),
+                ("moments_count", C.c_int64)]
 
 
 def _hipcc(out: str, sources: list, verbose: bool, force: bool, extra: tuple = ()) -> str:

@@ -18,6 +18,8 @@
 //    norm clip and the Adam step; ackppo_epoch runs a whole epoch of minibatches in one host
 //    call. No host round trip inside an update.
 #include <dlfcn.h>
+
+#include <chrono>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <rccl/rccl.h>
@@ -2019,6 +2021,12 @@ int ackppo_train(const ackppo_train_desc* d, void* stream) {
     return fail(ACKPPO_EINVAL, "ackppo_train: world > 1 needs an all-reduce hook, a hook needs the moments buffer");
   float* wimg = d->weight_image;
   const int S = d->n_idx, B = d->batch, nmb = (S + B - 1) / B;
+  // the moments layout a hook uses: [3][n_epochs][nmb] with the all-epoch buffers, else [3][nmb];
+  // the caller states the buffer's size, so a buffer sized for the per-epoch layout is refused, not
+  // overrun
+  const int64_t need_moments = 3 * (int64_t)nmb * ((d->perm_epochs && d->stats_epochs) ? d->n_epochs : 1);
+  if (dp && d->moments_count < need_moments)
+    return fail(ACKPPO_EINVAL, "ackppo_train: moments_count smaller than the hook's moments layout needs");
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d->loss_acc, 0, ACKPPO_NLOSS * sizeof(float), st) != hipSuccess)
     return fail(ACKPPO_EHIP, "ackppo_train: hipMemsetAsync(loss_acc)");
@@ -2116,6 +2124,7 @@ struct Rccl {
   decltype(&ncclAllReduce) allreduce = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) errstr = nullptr;
+  decltype(&ncclCommGetAsyncError) async_err = nullptr;
   bool ok = false;
 };
 Rccl& rccl() {
@@ -2130,7 +2139,8 @@ Rccl& rccl() {
     x.allreduce = (decltype(x.allreduce))dlsym(h, "ncclAllReduce");
     x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
     x.errstr = (decltype(x.errstr))dlsym(h, "ncclGetErrorString");
-    x.ok = x.get_id && x.init && x.allreduce && x.destroy && x.errstr;
+    x.async_err = (decltype(x.async_err))dlsym(h, "ncclCommGetAsyncError");
+    x.ok = x.get_id && x.init && x.allreduce && x.destroy && x.errstr && x.async_err;
     return x;
   }();
   return r;
@@ -2138,6 +2148,19 @@ Rccl& rccl() {
 int rccl_fail(const char* what, ncclResult_t r) {
   snprintf(g_err, sizeof g_err, "%s: %s", what, rccl().errstr ? rccl().errstr(r) : "RCCL error");
   return ACKPPO_EHIP;
+}
+// A non-blocking communicator (ncclConfig_t::blocking = 0, e.g. one torch built with
+// TORCH_NCCL_USE_COMM_NONBLOCKING) may return ncclInProgress from an enqueue: the call is then
+// still being issued, and ncclCommGetAsyncError reports ncclInProgress until it is done. Poll it
+// (bounded: 60 s of host time, then an error -- never a silent success).
+ncclResult_t rccl_settle(ncclComm_t comm, ncclResult_t r) {
+  if (r != ncclInProgress) return r;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (rccl().async_err(comm, &r) != ncclSuccess) return ncclInternalError;
+    if (r == ncclInProgress && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return ncclInProgress;
+  }
+  return r;
 }
 }  // namespace
 
@@ -2160,7 +2183,7 @@ int ackppo_rccl_init(const void* id128, int nranks, int rank, void** comm) {
   memcpy(&id, id128, sizeof id);
   ncclComm_t c = nullptr;
   const ncclResult_t r = rccl().init(&c, nranks, id, rank);
-  if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);
+  if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);  // a blocking communicator (no config)
   *comm = c;
   return ACKPPO_OK;
 }
@@ -2169,8 +2192,9 @@ int ackppo_rccl_allreduce(void* buf, int64_t count, int dtype, void* comm, void*
   if (!buf || !comm || count < 0 || (dtype != ACKPPO_F32 && dtype != ACKPPO_F64))
     return fail(ACKPPO_EINVAL, "ackppo_rccl_allreduce: bad arguments");
   if (!rccl().ok) return fail(ACKPPO_EHIP, "ackppo_rccl_allreduce: no librccl.so.1 loaded in this process");
-  const ncclResult_t r = rccl().allreduce(buf, buf, (size_t)count, dtype == ACKPPO_F32 ? ncclFloat32 : ncclFloat64,
-                                          ncclSum, (ncclComm_t)comm, (hipStream_t)stream);
+  const ncclResult_t r = rccl_settle(
+      (ncclComm_t)comm, rccl().allreduce(buf, buf, (size_t)count, dtype == ACKPPO_F32 ? ncclFloat32 : ncclFloat64,
+                                         ncclSum, (ncclComm_t)comm, (hipStream_t)stream));
   return r == ncclSuccess ? ACKPPO_OK : rccl_fail("ncclAllReduce", r);
 }
 

@@ -184,7 +184,7 @@ class PPO:
         self.perm_epochs = torch.empty(self.n_epochs, self.n_steps * self.n_envs, dtype=torch.int32, device=dev)
         self.stats_epochs = torch.zeros(self.n_epochs, nmb, 2, **f32)
         # the all-reduce hook of the data-parallel update (shard.TrainerCollective): on GPU nodes RCCL on
-        # torch's own communicator ("torch", the default) or on libackppo's ("rccl", opt-in); host-staged in
+        # libackppo's own communicator ("rccl", the default) or on torch's ("torch", opt-in); host-staged in
         # gloo rehearsals; a kind at world 1 runs the data-parallel path over one rank (timing it on one GPU)
         self.collective = None
         self._desc = self._train_desc()
@@ -299,6 +299,7 @@ class PPO:
         d.n_idx, d.batch = self.n_steps * self.n_envs, self.batch_size
         d.params, d.exp_avg, d.exp_avg_sq = (t.data_ptr() for t in (self.params, self.exp_avg, self.exp_avg_sq))
         d.perm, d.stats, d.moments = self.perm.data_ptr(), self.mb_stats.data_ptr(), self.mb_moments.data_ptr()
+        d.moments_count = self.mb_moments.numel()
         self.set_epoch_buffers(True, d)
         d.grad_partial, d.loss_partial = self.gpart.data_ptr(), self.lpart.data_ptr()
         d.grad, d.loss_acc, d.grad_norm_out = self.grad.data_ptr(), self.loss_acc.data_ptr(), self.gnorm.data_ptr()
@@ -326,7 +327,7 @@ class PPO:
 
     def set_collective(self, kind: str | None):
         """The update's all-reduce hook (shard.TrainerCollective): "torch", "rccl", "host", None = the
-        backend's default at world > 1 ("torch" on RCCL, "host" on gloo), or no hook at all at world 1."""
+        backend's default at world > 1 ("rccl" on RCCL, "host" on gloo), or no hook at all at world 1."""
         if self.collective is not None:
             self.collective.close()
             self.collective = None

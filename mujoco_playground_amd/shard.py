@@ -130,15 +130,16 @@ class TrainerCollective:
     step (include/ackppo.h ackppo_allreduce_fn), so a data-parallel PPO update is one C call per
     train() with no per-minibatch host round trip.
 
-    kind "torch" (default on the nccl = RCCL backend): ackppo_rccl_allreduce on the communicator of
+    kind "rccl" (default on the nccl = RCCL backend): a communicator of libackppo's own (ackppo_rccl_*)
+      over the ranks of the default process group (its unique id broadcast once over that group), or
+      over this process alone at world 1 (a one-rank communicator: the data-parallel path with real
+      RCCL calls, for timing it on one GPU). The standard RCCL pattern: ncclCommInitRank from a
+      unique id, every collective enqueued from C on the trainer's stream.
+    kind "torch" (opt-in until it has run on a multi-GPU node): ackppo_rccl_allreduce on the communicator of
       torch's own ProcessGroupNCCL (torch_rccl_comm): no second communicator, no unique-id exchange,
       and the RCCL library is checked to be the one torch loaded; each collective is enqueued from C
       on the trainer's stream (torch's current stream, so torch's later collectives on the same
       communicator are ordered after them on the device).
-    kind "rccl" (opt-in): a communicator of libackppo's own (ackppo_rccl_*) over the ranks of the
-      default process group (its unique id broadcast once over that group), or over this process
-      alone at world 1 (a one-rank communicator: the data-parallel path with real RCCL calls, for
-      timing it on one GPU).
     kind "host": a Python callback that all-reduces through torch.distributed on host copies --
       the gloo rehearsals (several ranks on one device, where RCCL cannot run); the callback
       synchronises the stream, so it is the slow path, for tests only. On an error it aborts the
@@ -150,7 +151,7 @@ class TrainerCollective:
 
         from . import _lib
         self.world, self.device = world, device
-        self.kind = kind or ("host" if _backend_is_gloo() else "torch")
+        self.kind = kind or ("host" if _backend_is_gloo() else "rccl")
         self.L = _lib.ppo_lib()
         self._bufs = {}
         self.comm = C.c_void_p()

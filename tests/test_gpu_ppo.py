@@ -322,8 +322,8 @@ def test_adv_moments_two_ranks_normalise_the_world_minibatch():
 
 def test_train_paths_bit_identical():
     """PPO.train is one ackppo_train call. Its single-rank sequence (no hook) and the data-parallel
-    sequence over one rank -- RCCL on torch's own communicator (kind "torch", the default at world > 1;
-    a one-rank nccl process group here), on libackppo's own communicator ("rccl") and the host-staged
+    sequence over one rank -- RCCL on libackppo's own communicator (kind "rccl", the default at world > 1),
+    on torch's own communicator ("torch"; a one-rank nccl process group here) and the host-staged
     hook (the gloo rehearsals' path, a no-op at world 1), each with every epoch's advantage moments
     formed at the start of the call (2 collectives per call) and with per-epoch moments -- give
     bit-identical parameters, Adam moments and loss statistics."""
@@ -332,7 +332,10 @@ def test_train_paths_bit_identical():
     from mujoco_playground_amd.rl.ppo import PPO
     made = False
     if not dist.is_initialized():
-        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device(DEV))
+        # the way shard.init builds it (no device_id: torch creates the communicator lazily, at the first
+        # collective on the rank's current device), so the communicator under test is the production one
+        torch.cuda.set_device(torch.device(DEV))
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
         made = True
     out = []
     try:
@@ -381,7 +384,7 @@ def _ppo_rank_rccl(rank, world, port, kind, q):
 
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs 2 GPUs")
 def test_ppo_data_parallel_rccl_two_gpus():
-    """Two ranks on two GPUs over RCCL (torch's communicator, the default; and libackppo's own): both
+    """Two ranks on two GPUs over RCCL (libackppo's own communicator, the default; and torch's): both
     ranks end with bit-identical parameters, equal to the host-hook (gloo) result of the same run."""
     import socket
     import torch.multiprocessing as mp
