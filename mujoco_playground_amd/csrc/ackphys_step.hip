@@ -266,14 +266,6 @@ __device__ __forceinline__ bool is_bad(float x) { return !(fabsf(x) <= 1e10f); }
 // v_rcp / v_rsq / v_sqrt forms. With SLP vectorisation on they made the register allocation worse
 // (36.7 -> 37.9 us/step contacts off); in the no-SLP build they measure faster (nc kernel 9.05 ->
 // 8.75 us, contacts on 69.2 -> 68.7 us; tools/variant_sweep.sh) and every parity test holds.
-// AK_HWMATH=0 restores the correctly rounded forms.
-#ifndef AK_HWMATH
-#define AK_HWMATH 1
-#endif
-#ifndef AK_POLYTRIG
-#define AK_POLYTRIG 1
-#endif
-#if AK_HWMATH  // hardware 1-ulp v_rcp / v_rsq / v_sqrt
 // An argument that is a compile-time constant once inlined (model constants: the constant blocks
 // of the mass matrix and of its factors, impedance and regulariser terms) takes the correctly
 // rounded form, which the compiler folds; the hardware builtins are opaque to constant folding and
@@ -286,18 +278,10 @@ __device__ __forceinline__ float fdiv(float a, float b) {
 __device__ __forceinline__ float frsq(float x) { return AK_HW_OR_FOLD(x, 1.0f / sqrtf(x), __builtin_amdgcn_rsqf(x)); }
 __device__ __forceinline__ float fsqrt(float x) { return AK_HW_OR_FOLD(x, sqrtf(x), __builtin_amdgcn_sqrtf(x)); }
 #define AK_PIVOT_RSQ(x) frsq(x)
-#else
-__device__ __forceinline__ float frcp(float x) { return 1.0f / x; }
-__device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
-__device__ __forceinline__ float frsq(float x) { return 1.0f / sqrtf(x); }
-__device__ __forceinline__ float fsqrt(float x) { return sqrtf(x); }
-#define AK_PIVOT_RSQ(x) __frsqrt_rn(x)
-#endif
 // sin / cos: the kernels' arguments are steer angles (|x| < ~0.7) and half rotation angles of one
 // step (|x| << 1), so when every lane's |x| <= pi/4 the wave takes the Cephes minimax polynomials of
 // that interval (the ones sincosf itself uses after its range reduction); otherwise sincosf.
 __device__ __forceinline__ void fsincos(float x, float& s, float& c) {
-#if AK_POLYTRIG
   if (__builtin_amdgcn_ballot_w64(!(fabsf(x) <= 0.785398163f)) == 0ull) {
     const float z = x * x;
     s = fmaf(x * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), x);
@@ -305,7 +289,6 @@ __device__ __forceinline__ void fsincos(float x, float& s, float& c) {
              fmaf(-0.5f, z, 1.0f));
     return;
   }
-#endif
   sincosf(x, &s, &c);
 }
 // wrap to [-pi, pi] (atan2(sin a, cos a) of the reference) for |a| <= 3 pi
@@ -570,31 +553,10 @@ __device__ __forceinline__ ObsOut observe(const float p[3], const float q[4], co
 // below are derived at compile time; skipped terms are structural zeros (0 * finite), so results
 // equal the dense factorisation up to the reordering's rounding.
 struct SymPat { bool nz[NV][NV]; };
-// per-mapping choice between the structured (KIND) and the dense (3) factorisation; picked by
-// measurement (tools/variant_sweep.sh): the lane kernel is faster structured, the quad kernels dense
-#ifndef AK_LANE_DENSE
-#define AK_LANE_DENSE 0
-#endif
-#ifndef AK_QUAD_DENSE
-#define AK_QUAD_DENSE 0  // measured (no-SLP build): structured 69.3 us vs dense 70.0 us per contacts-on step, obstacles 73.9 vs 76.3
-#endif
-#define LANE_K(k) (AK_LANE_DENSE ? 3 : (k))
-#ifndef AK_QUAD_START
-#define AK_QUAD_START 1  // quad kernels: Newton from qacc_smooth (0 = MuJoCo's start rule), see dynamics_quad()
-#endif
-#ifndef AK_NC_WARMSTART
-#define AK_NC_WARMSTART 1  // contacts-off kernel: Newton starts from qacc_warmstart (see dynamics())
-#endif
-#ifndef AK_NC_PREDICT
-#define AK_NC_PREDICT 1  // contacts-off kernel: first solve on a predicted active set (see dynamics())
-#endif
-#define QUAD_K(k) (AK_QUAD_DENSE ? 3 : (k))
-#ifdef AK_ORD_IDENT
-constexpr int ORD[NV] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
-#else
+// Every kernel factors structured (measured against the dense kind 3 in rounds 1-2: contacts on
+// 69.3 vs 70.0 us per step, obstacles 73.9 vs 76.3 us; the lane kernel faster structured too).
 constexpr int ORD[NV] = {W_SPIN_DOF[0], W_SPIN_DOF[1], W_SPIN_DOF[2], W_SPIN_DOF[3], W_STEER_DOF[2],
                          W_STEER_DOF[3], 0, 1, 2, 3, 4, 5};
-#endif
 static_assert(W_STEER_DOF[0] < 0 && W_STEER_DOF[1] < 0 && W_STEER_DOF[2] >= 6 && W_STEER_DOF[3] >= 6,
               "factorisation order assumes rear wheels without steering and two steered front wheels");
 constexpr bool ord_is_perm() {
@@ -612,10 +574,6 @@ constexpr SymPat make_pat(int kind) {
   SymPat p{};
   auto set = [&p](int a, int b) { p.nz[a][b] = true; p.nz[b][a] = true; };
   for (int i = 0; i < NV; i++) set(i, i);
-  if (kind == 3) {  // dense (the factorisation still runs in ORD order)
-    for (int i = 0; i < NV; i++)
-      for (int j = 0; j < NV; j++) set(i, j);
-  }
   for (int a = 3; a < 6; a++)
     for (int b = 0; b < 6; b++) set(a, b);  // I_O and m [c]x
   for (int w = 0; w < 4; w++) {
@@ -650,8 +608,8 @@ constexpr SymPat make_lpat(int kind) {
           if (l.nz[j][k]) l.nz[i][j] = true;
   return l;
 }
-constexpr SymPat PAT[4] = {make_pat(0), make_pat(1), make_pat(2), make_pat(3)};
-constexpr SymPat LPAT[4] = {make_lpat(0), make_lpat(1), make_lpat(2), make_lpat(3)};
+constexpr SymPat PAT[3] = {make_pat(0), make_pat(1), make_pat(2)};
+constexpr SymPat LPAT[3] = {make_lpat(0), make_lpat(1), make_lpat(2)};
 constexpr bool no_fill(int kind) {  // the order creates no fill outside the free-joint block
   for (int i = 0; i < NV; i++)
     for (int j = 0; j < i; j++)
@@ -1409,14 +1367,13 @@ __device__ __forceinline__ void xch_get(const float* x, int slot, int stride, Sc
 // The implicit-Euler factor chol(M + h diag(damping)) depends on the steer angles alone (M is
 // constant but for the front spin axes), so the prep wave computes it beside the solve and hands
 // its structural nonzeros over (float4 per lane: 16-byte LDS reads, conflict-free).
-constexpr int eu_words(int kind = LANE_K(0)) {
+constexpr int eu_words(int kind = 0) {
   int n = 0;
   for (int i = 0; i < NV; i++)
     for (int j = 0; j <= i; j++) n += LPAT[kind].nz[i][j] ? 1 : 0;
   return n;
 }
 constexpr int EU_VEC = (eu_words() + 3) / 4;
-constexpr int XH_VEC = (eu_words(LANE_K(1)) + 3) / 4;  // the typical piece's factor (XH)
 // chol(M) (EU = false: qacc_smooth) or chol(M + h diag(damping)) (EU: implicit Euler) at the
 // front steer angles d2, d3
 template <bool EU>
@@ -1433,12 +1390,12 @@ __device__ __forceinline__ void mass_factor(float d2, float d3, float L[NV][NV])
 #pragma unroll
     for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
   }
-  chol_sp<LANE_K(0)>(L);
+  chol_sp<0>(L);
 }
 __device__ __forceinline__ void euler_factor(const float qpos[13], float L[NV][NV]) {
   mass_factor<true>(qpos[W_STEER_QPOS[2]], qpos[W_STEER_QPOS[3]], L);
 }
-template <int KIND = LANE_K(0), int NVEC = EU_VEC>
+template <int KIND = 0, int NVEC = EU_VEC>
 __device__ __forceinline__ void eu_put(float* x, int lane, const float L[NV][NV]) {
   float w[4 * NVEC];
   int n = 0;
@@ -1453,7 +1410,7 @@ __device__ __forceinline__ void eu_put(float* x, int lane, const float L[NV][NV]
 #pragma unroll
   for (int v = 0; v < NVEC; v++) x4[v * 64 + lane] = make_float4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
 }
-template <int KIND = LANE_K(0), int NVEC = EU_VEC>
+template <int KIND = 0, int NVEC = EU_VEC>
 __device__ __forceinline__ void eu_get(const float* x, int lane, float L[NV][NV]) {
   float w[4 * NVEC];
   const float4* x4 = reinterpret_cast<const float4*>(x);
@@ -1470,26 +1427,6 @@ __device__ __forceinline__ void eu_get(const float* x, int lane, float L[NV][NV]
       if (LPAT[KIND].nz[i][j]) AK_F(L, i, j) = w[n++];
 }
 
-// Contacts-off kernel, typical predicted piece (AK_XH): the quadratic rows of the predicted piece
-// are, in ~99.8 % of env-steps, the steering equality and the friction-loss rows of the two
-// free-rolling front spins (tools/probes/active_set_probe.py). The piece's Hessian
-// H = M + sum over those rows of D J^T J depends on the steer angles and the rows' D alone, so the
-// prep wave builds and factors it beside the dynamics wave (same arithmetic, same order as
-// dyn_post's build); a wave whose lanes all predicted exactly that set takes the factor from LDS.
-constexpr uint32_t xh_rows() {
-  uint32_t m = 1u;  // row 0: the joint equality
-  for (int w = 2; w < 4; w++) m |= 1u << (W_SPIN_DOF[w] - 5);  // front-spin friction-loss rows
-  return m;
-}
-constexpr uint32_t XH_ROWS = xh_rows();
-// the rows of the typical piece that exist for this env (inactive rows add nothing to H)
-__device__ __forceinline__ uint32_t xh_mask(const bool sact[NSCAL]) {
-  uint32_t m = 0u;
-#pragma unroll
-  for (int r = 0; r < NSCAL; r++)
-    if (((XH_ROWS >> r) & 1u) && sact[r]) m |= 1u << r;
-  return m;
-}
 // H of the piece whose quadratic rows are qmask, lower triangle, as dyn_post builds it
 __device__ __forceinline__ void piece_hessian(const float M[NV][NV], uint32_t qmask, const float sD[NSCAL], float eqc2,
                                               float H[NV][NV]) {
@@ -1523,7 +1460,6 @@ struct DynPre {
   float sa[2][3], cyl[2][3];
   Solver sv;  // M; fs = -bias - damping (actuator forces added in dyn_post)
 };
-template <bool BIAS = true>  // BIAS = false: fs (bias + passive) comes from the observation wave (AK_XB)
 __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV], const float R[9], DynPre& P) {
   // front steer angles -> spin / cylinder axes in the chassis frame
 #pragma unroll
@@ -1536,39 +1472,30 @@ __device__ __forceinline__ void dyn_pre(const float qpos[13], const float u[NV],
   }
   STAMP(2);
   build_M(P.sv.M, P.sa);
-  if constexpr (BIAS) {
-    float b[NV];
-    bias(u, R, P.sa, b);
-    // passive damping (mj_passive)
+  float b[NV];
+  bias(u, R, P.sa, b);
+  // passive damping (mj_passive)
 #pragma unroll
-    for (int i = 0; i < NV; i++) P.sv.fs[i] = -b[i] - DAMPING[i] * u[i];
-  }
+  for (int i = 0; i < NV; i++) P.sv.fs[i] = -b[i] - DAMPING[i] * u[i];
 }
 
 // forward dynamics, second part: actuators, qacc_smooth, constraints and solve, Euler force
 // XEU / XM: the Euler / mass-matrix factor comes from another wave (eh / mh), see step_split
-// XH: the typical predicted piece's factor comes from the prep wave (hh) for lanes with hok
-// XB (with XM): fs = -bias - damping u comes with the mass-matrix factor, at fsx[i * 64]
-template <int NC, bool XEU = false, bool XM = false, bool XH = false, bool XB = false>  // NC = 1: contacts off
+template <int NC, bool XEU = false, bool XM = false>  // NC = 1: contacts off
 __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[13], const float u[NV],
                                          const float warm_u[NV], const float R[9], const float ctrl[3], uint32_t flags,
                                          const ScalRows& sr, StepResult& out, EuHand eh = EuHand{},
-                                         EuHand mh = EuHand{}, EuHand hh = EuHand{}, bool hok = false,
-                                         const float* fsx = nullptr) {
-  static_assert(!XB || XM, "fs is handed over with the mass-matrix factor");
+                                         EuHand mh = EuHand{}) {
   float(&sa)[2][3] = P.sa;
   float(&cyl)[2][3] = P.cyl;
   Solver& sv = P.sv;
   (void)sa;
-  float fact[3];  // XB: actuator forces, added once fs has arrived
-  (void)fact;
   {  // actuators (mj_fwdActuation)
     float c0 = ctrl[0];
     if (ACT_CTRLLIMITED[0]) c0 = fminf(fmaxf(c0, ACT_CTRLRANGE[0][0]), ACT_CTRLRANGE[0][1]);
     float f0 = ACT_GAIN[0] * c0 + ACT_BIAS1[0] * qpos[ACT_STEER_QPOS] + ACT_BIAS2[0] * u[ACT_STEER_DOF];
     if (ACT_FORCELIMITED[0]) f0 = fminf(fmaxf(f0, ACT_FORCERANGE[0][0]), ACT_FORCERANGE[0][1]);
-    if constexpr (!XB) sv.fs[ACT_STEER_DOF] += f0;
-    else fact[0] = f0;
+    sv.fs[ACT_STEER_DOF] += f0;
     float c1 = ctrl[1], c2 = ctrl[2];
     if (ACT_CTRLLIMITED[1]) c1 = fminf(fmaxf(c1, ACT_CTRLRANGE[1][0]), ACT_CTRLRANGE[1][1]);
     if (ACT_CTRLLIMITED[2]) c2 = fminf(fmaxf(c2, ACT_CTRLRANGE[2][0]), ACT_CTRLRANGE[2][1]);
@@ -1576,36 +1503,24 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     float f2 = ACT_GAIN[2] * c2 + ACT_BIAS2[2] * u[ACT_RR_DOF];
     if (ACT_FORCELIMITED[1]) f1 = fminf(fmaxf(f1, ACT_FORCERANGE[1][0]), ACT_FORCERANGE[1][1]);
     if (ACT_FORCELIMITED[2]) f2 = fminf(fmaxf(f2, ACT_FORCERANGE[2][0]), ACT_FORCERANGE[2][1]);
-    if constexpr (!XB) {
-      sv.fs[ACT_RL_DOF] += f1;
-      sv.fs[ACT_RR_DOF] += f2;
-    } else {
-      fact[1] = f1;
-      fact[2] = f2;
-    }
+    sv.fs[ACT_RL_DOF] += f1;
+    sv.fs[ACT_RR_DOF] += f2;
   }
   // qacc_smooth = M^-1 fs
   float L[NV][NV];
   if constexpr (XM) {  // factored by the observation wave (same steer angles)
     while (__hip_atomic_load(mh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
     eu_get(mh.x, mh.lane, L);
-    if constexpr (XB) {  // bias + passive from the observation wave, then the actuator forces as above
-#pragma unroll
-      for (int i = 0; i < NV; i++) sv.fs[i] = fsx[i * 64];
-      sv.fs[ACT_STEER_DOF] += fact[0];
-      sv.fs[ACT_RL_DOF] += fact[1];
-      sv.fs[ACT_RR_DOF] += fact[2];
-    }
   } else {
 #pragma unroll
     for (int i = 0; i < NV; i++)
 #pragma unroll
       for (int j = 0; j < NV; j++) L[i][j] = sv.M[i][j];
-    chol_sp<LANE_K(0)>(L);
+    chol_sp<0>(L);
   }
 #pragma unroll
   for (int i = 0; i < NV; i++) sv.a0[i] = sv.fs[i];
-  chol_sp_solve<LANE_K(0)>(L, sv.a0);
+  chol_sp_solve<0>(L, sv.a0);
 
   STAMP(3);
   // contacts
@@ -1671,7 +1586,7 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     float dw[NV], Mdw[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) dw[i] = warm_u[i] - sv.a0[i];
-    symv_M<LANE_K(0)>(sv.M, dw, Mdw);
+    symv_M<0>(sv.M, dw, Mdw);
 #pragma unroll
     for (int i = 0; i < NV; i++) cost_w += 0.5f * dw[i] * Mdw[i];
 #pragma unroll
@@ -1709,13 +1624,13 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     }
     cost_s += cs_c;
     // Newton start. MuJoCo takes the cheaper of qacc_warmstart and qacc_smooth; the contacts-off
-    // kernel starts from qacc_warmstart (AK_NC_WARMSTART): the cost is strictly convex (M > 0), so
+    // kernel starts from qacc_warmstart : the cost is strictly convex (M > 0), so
     // both starts reach the same unique minimiser -- the parity tests hold it to the oracle, which
     // applies MuJoCo's rule -- and on the benchmark workload the oracle's rule picks qacc_smooth
     // for 85 % of env-steps, from where Newton needs one more iteration (wave max 3 vs 2). With
     // contacts (stiff, ill-conditioned in f32) the f32 solve's last digits depend on the start, so
     // the contact kernels keep MuJoCo's rule.
-    const bool use_w = (NC && AK_NC_WARMSTART) ? true : cost_w < cost_s;
+    const bool use_w = NC ? true : cost_w < cost_s;
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] = use_w ? warm_u[i] : sv.a0[i];
     if (!use_w) {
@@ -1739,7 +1654,7 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
 #ifdef AK_STAMPS
   int diag_pair = 0;  // diag build: 1 = this lane's one-dof steer guess was inconsistent (9-pair search)
 #endif
-  if constexpr (NC && AK_NC_PREDICT) {
+  if constexpr (NC) {
     float ap[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) ap[i] = sv.a0[i];
@@ -1817,19 +1732,12 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
       if (d2 >= 0) grad[d2] -= f * eqc2;
       if (quad) qmask |= 1u << r;
     }
-    // the typical piece (every lane of the wave): factored by the prep wave (AK_XH)
-    const bool typ = XH && hok && qmask == xh_mask(sact);
-    if (XH && __builtin_amdgcn_ballot_w64(!typ) == 0ull) {
-      while (__hip_atomic_load(hh.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
-      eu_get<LANE_K(1), XH_VEC>(hh.x, hh.lane, H);
-    } else {
-      piece_hessian(sv.M, qmask, sD, eqc2, H);
-      chol_sp<LANE_K(1)>(H);
-    }
+    piece_hessian(sv.M, qmask, sD, eqc2, H);
+    chol_sp<1>(H);
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
-    chol_sp_solve<LANE_K(1)>(H, pdir);
+    chol_sp_solve<1>(H, pdir);
 #pragma unroll
     for (int i = 0; i < NV; i++) a[i] += pdir[i];
     int changed = 0;
@@ -1871,7 +1779,7 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
       float da[NV];
 #pragma unroll
       for (int i = 0; i < NV; i++) da[i] = a[i] - sv.a0[i];
-      symv_M<LANE_K(0)>(sv.M, da, grad);
+      symv_M<0>(sv.M, da, grad);
 #pragma unroll
       for (int i = 0; i < NV; i++) gscale = fmaxf(gscale, fabsf(grad[i]));
     }
@@ -1909,13 +1817,13 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     if constexpr (!NC) { FOR_CHAINS(slot_loop_hess, S, dirs, sa, H, grad); }
     (void)gscale;
     NT_MARK(0);
-    if (wm) chol_sp<LANE_K(2)>(H);  // wave-uniform: contact rows present in some lane
-    else chol_sp<LANE_K(1)>(H);
+    if (wm) chol_sp<2>(H);  // wave-uniform: contact rows present in some lane
+    else chol_sp<1>(H);
     float pdir[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) pdir[i] = -grad[i];
-    if (wm) chol_sp_solve<LANE_K(2)>(H, pdir);
-    else chol_sp_solve<LANE_K(1)>(H, pdir);
+    if (wm) chol_sp_solve<2>(H, pdir);
+    else chol_sp_solve<1>(H, pdir);
     NT_MARK(1);
     // Jp for all rows
     if constexpr (!NC) { FOR_CHAINS(slot_loop_jp, S, dirs, sa, pdir); }
@@ -1923,7 +1831,7 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
     for (int r = 0; r < NSCAL; r++) sjp[r] = scal_J_dot(r, pdir);
     // exact line search on the piecewise-linear derivative phi'(alpha)
     float Mp[NV];
-    symv_M<LANE_K(0)>(sv.M, pdir, Mp);
+    symv_M<0>(sv.M, pdir, Mp);
     float pMp = 0.0f, pg0 = 0.0f;
 #pragma unroll
     for (int i = 0; i < NV; i++) { pMp += pdir[i] * Mp[i]; pg0 += Mp[i] * (a[i] - sv.a0[i]); }
@@ -2050,11 +1958,11 @@ __device__ __forceinline__ void dyn_post(Slots& S, DynPre& P, const float qpos[1
       for (int j = 0; j < NV; j++) L[i][j] = (j <= i) ? sv.M[i][j] : 0.0f;
 #pragma unroll
     for (int i = 0; i < NV; i++) L[i][i] += DT * DAMPING[i];
-    chol_sp<LANE_K(0)>(L);
+    chol_sp<0>(L);
   }
 #pragma unroll
   for (int i = 0; i < NV; i++) out.acce[i] = sv.fs[i] + fc[i];
-  chol_sp_solve<LANE_K(0)>(L, out.acce);
+  chol_sp_solve<0>(L, out.acce);
   bool bad = false;
 #pragma unroll
   for (int i = 0; i < NV; i++) bad |= is_bad(a[i]);
@@ -2296,38 +2204,16 @@ __device__ __forceinline__ bool any_redo(const uint8_t* sh_bad, int lane, int np
   return r;
 }
 
-#ifndef AK_XCH
-#define AK_XCH 1  // a third "prep" wave computes the controller and the scalar rows (LDS + flag)
-#endif
-#ifndef AK_XEU
-#define AK_XEU 1  // with AK_XCH: the prep wave also factors M + h diag(damping) for the Euler solve
-#endif
-#ifndef AK_PREP_RAYS
-#define AK_PREP_RAYS 40  // with AK_XCH: the prep wave also casts rays 10 .. AK_PREP_RAYS-1 (10: none)
-#endif
-#ifndef AK_XM
-#define AK_XM 1  // with AK_XCH: the observation wave factors M (qacc_smooth) before its observation
-#endif
-#ifndef AK_XH
-// with AK_XCH, contacts off: the prep wave factors the typical predicted piece (xh_rows). Measured
-// off (tools/variant_sweep.sh, rollout, 1000 steps): the dynamics wave gains ~300 cycles but the
-// prep wave's ~1.3k-cycle factorisation delays its rays past the observation wave's, which then
-// holds barrier 1: 4.52 -> 4.97 us per step (prep rays 10-39), 4.79 (10-31), 4.92 (10-27)
-#define AK_XH 0
-#endif
-#ifndef AK_XB
-// with AK_XM: the observation wave also computes fs = -bias - damping u (off the dynamics wave).
-// Measured off (tools/variant_sweep.sh, rollout, 1000 steps): 4.52 -> 5.03 us per contacts-off
-// step -- the observation wave's factor + bias arrive later than the dynamics wave's own bias
-#define AK_XB 0
-#endif
-static_assert(!AK_XB || AK_XM, "AK_XB hands fs over with the mass-matrix factor");
-static_assert(AK_XCH || (AK_PREP_RAYS == 10 && !AK_XEU && !AK_XM), "the hand-overs need the prep wave's exchange");
+// The lane kernels' helper waves, each measured faster than without it: a third
+// "prep" wave computes the controller and the scalar rows (LDS + flag), factors M + h diag(damping)
+// for the Euler solve (flag 2) and casts rays 10 .. PREP_RAYS-1; the observation wave factors M for
+// qacc_smooth (flag 3) before its observation. (Measured and dropped, rounds 2-3: the prep wave
+// factoring the typical predicted piece, 4.52 -> 4.79-4.97 us per step; the observation wave
+// computing the bias forces, 4.52 -> 5.03 us.)
+constexpr int PREP_RAYS = 40;
 constexpr int XEU_OFF = (XCH_WORDS + 1) * 64;  // float offset of the Euler factor words in xch
-constexpr int XM_OFF = XEU_OFF + (AK_XEU ? 4 * EU_VEC * 64 : 0);  // ... and of the mass-matrix factor
-constexpr int XH_OFF = XM_OFF + (AK_XM ? 4 * EU_VEC * 64 : 0);  // ... and of the typical piece's factor
-constexpr int XB_OFF = XH_OFF + (AK_XH ? 4 * XH_VEC * 64 : 0);  // ... and of fs (AK_XB)
-constexpr int XCH_FLOATS = XB_OFF + (AK_XB ? NV * 64 : 0);
+constexpr int XM_OFF = XEU_OFF + 4 * EU_VEC * 64;  // ... and of the mass-matrix factor
+constexpr int XCH_FLOATS = XM_OFF + 4 * EU_VEC * 64;
 
 template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
@@ -2343,10 +2229,8 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
   uint32_t step = 0, episode = 0;
   float R[9], u[NV], wu[NV], ctrl[3] = {0.0f, 0.0f, 0.0f};
   DynPre P;
-  if constexpr (AK_XCH) {
-    if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; xflag[4] = 0; }
-    __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
-  }
+  if (lane == 0) { xflag[0] = 0; xflag[1] = 0; xflag[2] = 0; xflag[3] = 0; xflag[4] = 0; }
+  __syncthreads();  // barrier 0: the exchange flags are clear before the prep wave can raise them
   const int sms = 64 * npair;  // word stride of the LDS state mirrors
   float* const smw = A.sm ? A.sm + slot : nullptr;
   float* const smn = A.sm_next ? A.sm_next + slot : nullptr;
@@ -2381,12 +2265,6 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
         smn[ST_EPIS * sms] = __uint_as_float(episode);
       }
     }
-    if constexpr (!AK_XCH) {
-      const Soa act = soa(A.action, 2, n);
-      const float a0 = ldf(act, 0, 2 * vo), a1 = ldf(act, 0, 2 * vo + 4);
-      bool badctrl;
-      controller(a0, a1, A.prm.max_linear_velocity, A.prm.max_angular_velocity, ctrl, badctrl);
-    }
     STAMP(1);
 #pragma unroll
     for (int i = 0; i < 13; i++) bad_state |= is_bad(qpos[i]);
@@ -2394,10 +2272,10 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
     if (bad_state) reset_to_qpos0(qpos, qvel, warm, ctrl);  // mj_checkPos / mj_checkVel -> mj_resetData
     to_u(qpos, qvel, warm, R, u, wu);
-    dyn_pre<!(AK_XCH && AK_XB)>(qpos, u, R, P);
+    dyn_pre(qpos, u, R, P);
   }
   ScalRows sr;
-  if constexpr (AK_XCH) {
+  {
     // the prep wave has put this env's controller output and scalar rows into LDS (computed from
     // the loaded state; an env reset for a bad state computes its own at qpos0): wait for its flag
     STAMP(20);
@@ -2409,16 +2287,11 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
     else {
       ctrl[0] = xc[0]; ctrl[1] = xc[1]; ctrl[2] = xc[2];
     }
-  } else if (valid) {
-    scalar_rows(qpos, u, sr);
   }
   if (valid) {
     StepResult res;
-    dyn_post<NC, AK_XEU != 0, AK_XM != 0, NC && AK_XH, AK_XB != 0>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res,
-                                                                  EuHand{xch + XEU_OFF, xflag + 2, lane},
-                                                                  EuHand{xch + XM_OFF, xflag + 3, lane},
-                                                                  EuHand{xch + XH_OFF, xflag + 4, lane}, !bad_state,
-                                                                  xch + XB_OFF + lane);
+    dyn_post<NC, true, true>(S, P, qpos, u, wu, R, ctrl, A.flags, sr, res, EuHand{xch + XEU_OFF, xflag + 2, lane},
+                             EuHand{xch + XM_OFF, xflag + 3, lane});
     if (res.bad) {  // mj_checkAcc: mj_resetData and the step redone from qpos0 (rare)
       bad_state = redo = true;
       reset_to_qpos0(qpos, qvel, warm, ctrl);
@@ -2467,7 +2340,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
 __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad,
                                               uint8_t* sh_reset, int lane, int e, bool valid, int slot, int npair) {
   STAMP_SCOPE
-  if constexpr (AK_XCH) __syncthreads();  // barrier 0 (see step_dyn_wave)
+  __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
   const Soa st = soa(A.state, NSTATE, n);
@@ -2511,29 +2384,12 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
 #pragma unroll
     for (int i = 0; i < NV; i++) bad_state |= is_bad(qvel[i]);
   }
-  if constexpr (AK_XM) {  // chol(M) for the dynamics wave's qacc_smooth, at qpos0 for a reset state
+  {  // chol(M) for the dynamics wave's qacc_smooth, at qpos0 for a reset state
     if (valid) {
       float L[NV][NV];
       mass_factor<false>(bad_state ? QPOS0[W_STEER_QPOS[2]] : qpos[W_STEER_QPOS[2]],
                          bad_state ? QPOS0[W_STEER_QPOS[3]] : qpos[W_STEER_QPOS[3]], L);
       eu_put(xch + XM_OFF, lane, L);
-      if constexpr (AK_XB) {  // fs = -bias - damping u of the (reset) state, as dyn_pre computes it
-        float qp[13], qv[NV], wz[NV], R[9], u[NV], wu[NV], sa[2][3], b[NV];
-#pragma unroll
-        for (int i = 0; i < 13; i++) qp[i] = bad_state ? QPOS0[i] : qpos[i];
-#pragma unroll
-        for (int i = 0; i < NV; i++) { qv[i] = bad_state ? 0.0f : qvel[i]; wz[i] = 0.0f; }
-        to_u(qp, qv, wz, R, u, wu);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; s2++) {
-          float c, sn;
-          fsincos(qp[W_STEER_QPOS[2 + s2]], sn, c);
-          rot_axis(sa[s2], S_AXIS[s2], W_SPIN_AXIS[2 + s2], c, sn);
-        }
-        bias(u, R, sa, b);
-#pragma unroll
-        for (int i = 0; i < NV; i++) xch[XB_OFF + i * 64 + lane] = -b[i] - DAMPING[i] * u[i];
-      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(xflag + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2555,7 +2411,7 @@ __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xf
       float R[9];
       quat_R(q, R);
       if (pass == 0) {
-        o = observe<0, AK_PREP_RAYS>(p, q, R, gx, gy, ref, obs, vo, A.prm, [&]() __attribute__((always_inline)) {
+        o = observe<0, PREP_RAYS>(p, q, R, gx, gy, ref, obs, vo, A.prm, [&]() __attribute__((always_inline)) {
           // the prep wave's rays: written to obs and their minimum to LDS before it raised flag 1
           while (__hip_atomic_load(xflag + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
             __builtin_amdgcn_s_sleep(1);
@@ -2608,11 +2464,11 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
   step_serial(A, lds, lane, e);
 }
 
-// Prep wave (AK_XCH): the controller (float64) and the scalar constraint rows of the same 64 envs,
+// Prep wave: the controller (float64) and the scalar constraint rows of the same 64 envs,
 // off the dynamics wave's critical path -- they need only the action and the hinge positions and
 // speeds. Handed over through LDS and a workgroup-scope release / acquire flag (no barrier: the
-// observation wave must not wait for it). Then (AK_XEU) the implicit-Euler factor, which the
-// dynamics wave needs only after its solve (flag 2), and (AK_PREP_RAYS) rangefinders for the
+// observation wave must not wait for it). Then the implicit-Euler factor, which the
+// dynamics wave needs only after its solve (flag 2), and (PREP_RAYS) rangefinders for the
 // observation wave (flag 1); the wave joins barriers 1 and 2 and exits.
 template <int NC>
 __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad, int lane,
@@ -2668,25 +2524,7 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
 #pragma unroll
     for (int i = 0; i < 13; i++) qpos[i] = QPOS0[i];
   }
-  if constexpr (NC && AK_XH) {  // the typical predicted piece's factor (flag 4; unused by reset lanes)
-    if (valid) {
-      float sa[2][3];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; s2++) {
-        float c, sn;
-        fsincos(qpos[W_STEER_QPOS[2 + s2]], sn, c);
-        rot_axis(sa[s2], S_AXIS[s2], W_SPIN_AXIS[2 + s2], c, sn);
-      }
-      float M[NV][NV], H[NV][NV];
-      build_M(M, sa);
-      piece_hessian(M, xh_mask(sr.act), sr.D, sr.eqc2, H);
-      chol_sp<LANE_K(1)>(H);
-      eu_put<LANE_K(1), XH_VEC>(xch + XH_OFF, lane, H);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(xflag + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  if constexpr (AK_XEU) {
+  {
     if (valid) {
       float L[NV][NV];
       euler_factor(qpos, L);
@@ -2696,8 +2534,8 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
     if (lane == 0) __hip_atomic_store(xflag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     STAMP(16);
   }
-  if constexpr (AK_PREP_RAYS > 10) {
-    // rangefinders 10 .. AK_PREP_RAYS-1 of the observation (taken at the pre-integration pose, or at
+  {
+    // rangefinders 10 .. PREP_RAYS-1 of the observation (taken at the pre-integration pose, or at
     // qpos0 for a state mj_checkPos/Vel resets): stored here, their minimum handed to wave 1
     float mn = 3.0e38f;
     if (valid) {
@@ -2710,11 +2548,11 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
       const RayFrame F = ray_frame(p, R);
       if (__builtin_amdgcn_ballot_w64(!floor_rays_all_miss(p, R)) == 0ull) {
 #pragma unroll
-        for (int i = 10; i < AK_PREP_RAYS; i++) stf(obs, i, vo, -1.0f);
+        for (int i = 10; i < PREP_RAYS; i++) stf(obs, i, vo, -1.0f);
         mn = coll_reading(-1.0f, A.prm);
       } else {
 #pragma unroll
-        for (int i = 10; i < AK_PREP_RAYS; i++) {
+        for (int i = 10; i < PREP_RAYS; i++) {
           const float v = ray_floor_f(F, RAY_DIR[i][0], RAY_DIR[i][1]);
           stf(obs, i, vo, v);
           mn = fminf(mn, coll_reading(v, A.prm));
@@ -2741,13 +2579,13 @@ __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* x
 }
 
 // PW wave pairs per workgroup: waves 0..PW-1 run the dynamics of envs [64 w, 64 w + 64) of the
-// block, waves PW..2PW-1 their observations (2 PW waves on the CU's 4 SIMDs); with AK_XCH a
-// third wave (PW = 1) prepares the controller and scalar rows
+// block, waves PW..2PW-1 their observations (2 PW waves on the CU's 4 SIMDs); a third wave
+// (PW = 1) prepares the controller and scalar rows
 template <int NC, int PW>
 __device__ __forceinline__ void step_split(const Args& A) {
-  static_assert(!AK_XCH || PW == 1, "the prep wave serves one dynamics wave");
+  static_assert(PW == 1, "the prep wave serves one dynamics wave");
   __shared__ float lds[NC ? 1 : NSLOT * NF * 64];
-  __shared__ __attribute__((aligned(16))) float xch[AK_XCH ? XCH_FLOATS : 1];
+  __shared__ __attribute__((aligned(16))) float xch[XCH_FLOATS];
   __shared__ int xflag[5];
   __shared__ uint8_t sh_bad[64 * PW], sh_reset[64 * PW];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2759,16 +2597,13 @@ __device__ __forceinline__ void step_split(const Args& A) {
   else if (wave < 2 * PW) step_obs_wave(A, xch, xflag, sh_bad, sh_reset, lane, e, valid, slot, PW);
   else step_prep_wave<NC>(A, xch, xflag, sh_bad, lane, blockIdx.x * A.epw + lane, lane < A.epw && blockIdx.x * A.epw + lane < A.n);
 }
-#ifndef AK_NC_PW
-#define AK_NC_PW 1  // wave pairs per workgroup of the contacts-off kernel
-#endif
-constexpr int LANE_THREADS = 64 * (2 * AK_NC_PW + (AK_XCH ? 1 : 0));
-extern "C" __global__ void __launch_bounds__(64 * (2 + (AK_XCH ? 1 : 0)), 1) ackphys_step_kernel(Args A) {
+constexpr int LANE_THREADS = 64 * 3;  // dynamics, observation and prep wave
+extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_kernel(Args A) {
   step_split<0, 1>(A);
 }
 // contacts off (BASELINE configs[1]): the contact machinery is compiled out
 extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_kernel(Args A) {
-  step_split<1, AK_NC_PW>(A);
+  step_split<1, 1>(A);
 }
 
 // Rollout kernels (ackphys_rollout): A.ksteps consecutive steps of the same envs in one launch,
@@ -2777,35 +2612,28 @@ extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_step_nc_ke
 // the launch: dispatch, wave start-up and the drain of the whole grid. Step k + 1's prep and
 // observation waves load the state the dynamics wave stored in step k: with the prep wave that
 // store precedes barrier 0 of step k + 1, which the loading waves pass first (same CU, so the
-// workgroup-scope fence of the barrier suffices); without it an explicit barrier separates them.
-#ifndef AK_ROLL_SM
-#define AK_ROLL_SM 1  // lane rollout kernels: state between steps in an LDS mirror, not HBM
-#endif
+// workgroup-scope fence of the barrier suffices). Between steps the state lives in an LDS mirror
+// (double-buffered), not HBM; only the launch's last step stores it.
 template <int NC, int PW>
 __device__ __forceinline__ void rollout_split(const Args& A) {
-  __shared__ float sm[2][AK_ROLL_SM ? NSTATE * 64 * PW : 1];
-  __shared__ float nctrl[AK_ROLL_SM && AK_XCH ? 3 * 64 : 1];
+  __shared__ float sm[2][NSTATE * 64 * PW];
+  __shared__ float nctrl[3 * 64];
 #pragma unroll 1
   for (int k = 0; k < A.ksteps; k++) {
-    if (!AK_XCH && k) __syncthreads();
     Args B = step_args(A, k);
-    if constexpr (AK_ROLL_SM) {
-      B.sm = sm[k & 1];
-      B.sm_next = sm[(k + 1) & 1];
-      B.sm_in = k > 0;
-      B.sm_out = k + 1 < A.ksteps;
-      if constexpr (AK_XCH) {
-        B.nctrl = nctrl;
-        B.next_action = k + 1 < A.ksteps ? A.action + (size_t)(k + 1) * 2 * A.n : nullptr;
-      }
-    }
+    B.sm = sm[k & 1];
+    B.sm_next = sm[(k + 1) & 1];
+    B.sm_in = k > 0;
+    B.sm_out = k + 1 < A.ksteps;
+    B.nctrl = nctrl;
+    B.next_action = k + 1 < A.ksteps ? A.action + (size_t)(k + 1) * 2 * A.n : nullptr;
     step_split<NC, PW>(B);
   }
 }
 extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_rollout_nc_kernel(Args A) {
-  rollout_split<1, AK_NC_PW>(A);
+  rollout_split<1, 1>(A);
 }
-extern "C" __global__ void __launch_bounds__(64 * (2 + (AK_XCH ? 1 : 0)), 1) ackphys_rollout_kernel(Args A) {
+extern "C" __global__ void __launch_bounds__(LANE_THREADS, 1) ackphys_rollout_kernel(Args A) {
   rollout_split<0, 1>(A);
 }
 
@@ -3088,13 +2916,12 @@ static int launch_steps(ackphys_t* ctx, ak::Args a, uint32_t flags, void* stream
                          (hipStream_t)stream, a);
   } else {
     a.epw = ctx->variant == ACKPHYS_VARIANT_LANE16 ? 16 : 64;
-    const int pw = (flags & (ACKPHYS_POSTSTEP_OBS | ACKPHYS_CONTACTS)) ? 1 : AK_NC_PW;
-    int blocks = (ctx->n_env + a.epw * pw - 1) / (a.epw * pw);
+    int blocks = (ctx->n_env + a.epw - 1) / a.epw;
     if (flags & ACKPHYS_POSTSTEP_OBS)
       hipLaunchKernelGGL(ackphys_step_serial_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
     else if (flags & ACKPHYS_CONTACTS)
       hipLaunchKernelGGL(multi ? ackphys_rollout_kernel : ackphys_step_kernel, dim3(blocks),
-                         dim3(64 * (2 + (AK_XCH ? 1 : 0))), 0, (hipStream_t)stream, a);
+                         dim3(LANE_THREADS), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(multi ? ackphys_rollout_nc_kernel : ackphys_step_nc_kernel, dim3(blocks), dim3(LANE_THREADS),
                          0, (hipStream_t)stream, a);

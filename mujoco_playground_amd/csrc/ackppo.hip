@@ -30,12 +30,7 @@
 #include "../../include/ackppo.h"
 #include "ackppo_math.inc"
 
-#ifndef PP_UNROLL
-#define PP_UNROLL 2
-#endif
-#define PP_STR2(x) #x
-#define PP_STR(x) PP_STR2(x)
-#define PP_UNROLL_STR PP_STR(unroll PP_UNROLL)
+#define PP_UNROLL_STR "unroll 2"
 
 #ifdef PP_STAMPS
 __device__ unsigned long long* g_pp_stamps;
@@ -472,17 +467,10 @@ constexpr int X = TBASE, H1 = X + 80 * LDP, H2 = H1 + H * LDP, D2 = H2 + H * LDP
 constexpr int GA = D2 + H * LDP;      // actor: gmu [2][LDP], glog [2][LDP]; critic: gv [LDP]
 constexpr int TOTAL1 = GA + 4 * LDP;
 constexpr int TSZ = TOTAL1 - TBASE;  // one tile's region (X .. GA)
-// NT tiles per workgroup (AK_GRAD1_NT): 1 = 256 threads, two workgroups per CU; 2 = 512 threads,
-// the two tiles' waves share one staged copy of the net's weights and one partial row (half the
-// rows for ackppo_reduce), one workgroup per CU
-#ifndef AK_GRAD1_NT
-#define AK_GRAD1_NT 2
-#endif
-#ifndef AK_GRAD1_PREFETCH
-#define AK_GRAD1_PREFETCH 0
-#endif
-
-constexpr int NT = AK_GRAD1_NT;
+// NT tiles per workgroup: 512 threads, the two tiles' waves share one staged copy of the net's
+// weights and one partial row (half the rows for the reduction), one workgroup per CU (measured
+// against one 256-thread tile per workgroup, two workgroups per CU: 18.9 vs 19.9 us, round 4)
+constexpr int NT = 2;
 static_assert(NT == 1 || NT == 2, "one or two tiles per workgroup");
 constexpr int TOTAL = TBASE + NT * TSZ;
 static_assert(NT == 2 ? TOTAL * 4 <= 160 * 1024 : TOTAL * 4 * 2 <= 160 * 1024,
@@ -737,9 +725,6 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     gather_x(tile, row_idx(tile));
   };
 
-  // AK_GRAD1_PREFETCH: the first tile's gathers issued before the weight staging (their latency
-  // overlaps it; the registers they hold through the staging cost a few spill slots)
-  if (AK_GRAD1_PREFETCH && !IMG && grp0 < ngrp) loads(NT * grp0 + half);
   int hx = 0;  // grad1i: the first tile's heads sample index (loaded with the rows' index)
   if constexpr (IMG) {
     // the first tile's sample indices, then the weight image's LDS-DMA copies (no registers), then the
@@ -786,7 +771,7 @@ __device__ __forceinline__ void grad1(const GradArgs& A) {
     __syncthreads();  // the previous tile's LDS reads are done (and the weights staged)
     int sidx = hx;  // grad1i's first tile: X in LDS already, the heads' index loaded with the rows'
     if (!(IMG && grp == grp0)) {
-      if (!AK_GRAD1_PREFETCH || grp != grp0) loads(tile);
+      loads(tile);
       const int r = htid >> 3, q = htid & 7;
 #pragma unroll
       for (int i = 0; i < 10; i++) tb[X + (q * 10 + i) * LDP + r] = xg[i];
@@ -1399,90 +1384,58 @@ extern "C" __global__ void __launch_bounds__(ADV_THREADS) ackppo_perm_moments_ke
   }
 }
 
-// Two passes, no atomics, no scratch: (1) grid (param blocks of 256, RG row groups) sums rows
-// by, by + RG, ... with 4 loads in flight per thread and writes the sum IN PLACE into row by
-// (row by belongs to group by alone, and element (by, p) to one thread, which read it first);
-// (2) sums rows 0..RG-1. The caller-owned partial rows are the only buffer, so concurrent
-// learners on other streams or devices share nothing.
-// One-launch reduction (default): a 1024-thread block owns 64 x R1_V consecutive parameters; its
-// 16 waves each sum every 16th partial row of them (coalesced 1 KB row reads at R1_V = 4, every
-// row load in flight at once), the 16 sums are combined through LDS; block 0 also reduces the loss
-// rows. At R1_V = 4 the 18 764 parameters take 74 blocks (R1_V = 1: 294, more than one per CU).
-// It replaced the two-launch form below (row groups in place, then the group sums).
-#ifndef AK_PPO_REDUCE1
-#define AK_PPO_REDUCE1 1
-#endif
-#ifndef AK_PPO_R1VEC  // parameters per lane of the one-launch reduction (1, 2 or 4: float, float2, float4 loads)
-#define AK_PPO_R1VEC 1
-#endif
-constexpr int R1_P = 64, R1_G = 16, R1_V = AK_PPO_R1VEC, R1_PB = R1_P * R1_V;  // R1_PB parameters per block
-static_assert(P % R1_V == 0, "whole vectors per partial row");
-template <int V>
-struct R1Vec;
-template <>
-struct R1Vec<1> {
-  using T = float;
-  static __device__ __forceinline__ float at(const T& v, int) { return v; }
-};
-template <>
-struct R1Vec<2> {
-  using T = float2;
-  static __device__ __forceinline__ float at(const T& v, int c) { return c ? v.y : v.x; }
-};
-template <>
-struct R1Vec<4> {
-  using T = float4;
-  static __device__ __forceinline__ float at(const T& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w; }
-};
+// The reduction of the partial rows (the C-ABI ackppo_reduce): no atomics, no scratch. A
+// 1024-thread block owns 64 consecutive parameters; its 16 waves each sum every 16th partial row of
+// them (every row load in flight at once), the 16 sums are combined through LDS; block 0 also
+// reduces the loss rows. (It replaced a two-launch form, row groups in place then the group sums;
+// 2- and 4-parameter vector loads per lane measured slower, round 4.) The caller-owned partial rows
+// are the only buffer, so concurrent learners on other streams or devices share nothing.
+constexpr int R1_P = 64, R1_G = 16;  // parameters per block, row groups
 extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce1_kernel(const float* gpart, int nblk,
                                                                         const float* lpart, float ent_coef,
                                                                         float* grad, float* loss, int accumulate) {
-  // a block owns R1_PB consecutive parameters: lane pl of wave g loads R1_V of them (one vector
-  // load per partial row: 64 lanes x 4 floats = a 1 KB coalesced read) from every 16th row
-  using VT = typename R1Vec<R1_V>::T;
-  __shared__ float red[R1_G][R1_PB + 1];
+  // a block owns R1_P consecutive parameters: lane pl of wave g loads its one from every 16th row
+  __shared__ float red[R1_G][R1_P + 1];
   __shared__ float lred[256];
   const int tid = threadIdx.x, pl = tid & (R1_P - 1), g = tid / R1_P;
-  const int vidx = blockIdx.x * R1_P + pl;  // vector index
-  const bool vok = vidx < P / R1_V;
+  const int vidx = blockIdx.x * R1_P + pl;  // parameter index
+  const bool vok = vidx < P;
   // all R1_K of this thread's rows in flight at once (one memory latency, not four), then summed in
-  // the order of the original loop -- blocks of 4 rows into acc[0..3] while a whole block of 4
-  // remains, the tail rows into acc[0] -- per parameter the same order whatever R1_V is
+  // blocks of 4 rows into acc[0..3] while a whole block of 4 remains, the tail rows into acc[0]
   constexpr int R1_K = GRAD_MAX_BLOCKS / R1_G;
   static_assert(R1_K % 4 == 0, "row blocks of four");
-  VT x[R1_K];
+  float x[R1_K];
 #pragma unroll
   for (int k = 0; k < R1_K; k++) {
     const int b = g + k * R1_G;
-    x[k] = (vok && b < nblk) ? reinterpret_cast<const VT*>(gpart + (size_t)b * P)[vidx] : VT{};
+    x[k] = (vok && b < nblk) ? gpart[(size_t)b * P + vidx] : 0.0f;
   }
   int nmain = 0;  // blocks j with g + 4 R1_G j + 3 R1_G < nblk (a prefix)
 #pragma unroll
   for (int j = 0; j < R1_K / 4; j++) nmain += (g + 4 * R1_G * j + 3 * R1_G < nblk) ? 1 : 0;
-#pragma unroll
-  for (int c = 0; c < R1_V; c++) {
+  {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < R1_K / 4; j++)
       if (j < nmain) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc[i] += R1Vec<R1_V>::at(x[4 * j + i], c);
+        for (int i = 0; i < 4; i++) acc[i] += x[4 * j + i];
       }
 #pragma unroll
     for (int k = 0; k < R1_K; k++)
-      if (k >= 4 * nmain) acc[0] += R1Vec<R1_V>::at(x[k], c);  // rows past nblk are 0.0f: adding them changes nothing
-    red[g][R1_V * pl + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      if (k >= 4 * nmain) acc[0] += x[k];  // rows past nblk are 0.0f: adding them changes nothing
+    red[g][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
   __syncthreads();
-  const int pidx = blockIdx.x * R1_PB + tid;
-  if (tid < R1_PB && pidx < P) {
+  const int pidx = blockIdx.x * R1_P + tid;
+  if (tid < R1_P && pidx < P) {
     float s = 0.0f;
 #pragma unroll
     for (int k = 0; k < R1_G; k++) s += red[k][tid];
     if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
     grad[pidx] = s;
   }
-  if (blockIdx.x == 0) {  // loss rows: as ackppo_reduce_kernel, on the block's first 256 threads
+  if (blockIdx.x == 0) {  // loss rows (32 block-strided groups x 8 slots, then an LDS tree), on the block's first 256 threads
     static_assert(ACKPPO_NLOSS == 8, "loss row layout");
     const int slot = tid & 7, grp = tid >> 3;
     float s = 0.0f;
@@ -1495,49 +1448,6 @@ extern "C" __global__ void __launch_bounds__(1024) ackppo_reduce1_kernel(const f
       __syncthreads();
     }
     if (tid < ACKPPO_NLOSS) loss[tid] = (accumulate ? loss[tid] : 0.0f) + lred[tid];
-  }
-}
-
-constexpr int REDUCE_RG = 16;
-extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_rows_kernel(float* gpart, int nblk) {
-  const int pidx = blockIdx.x * 256 + threadIdx.x;
-  const int rg = gridDim.y, by = blockIdx.y;
-  if (pidx >= P) return;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  int b = by;
-  for (; b + 3 * rg < nblk; b += 4 * rg) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) acc[i] += gpart[(size_t)(b + i * rg) * P + pidx];
-  }
-  for (; b < nblk; b += rg) acc[0] += gpart[(size_t)b * P + pidx];
-  gpart[(size_t)by * P + pidx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-}
-extern "C" __global__ void __launch_bounds__(256) ackppo_reduce_kernel(const float* tmp, int rg, const float* lpart,
-                                                                       int nblk, float ent_coef, float* grad,
-                                                                       float* loss, int accumulate) {
-  const int pidx = blockIdx.x * 256 + threadIdx.x;
-  if (pidx < P) {
-    float s = 0.0f;
-#pragma unroll 4
-    for (int r = 0; r < rg; r++) s += tmp[(size_t)r * P + pidx];
-    if (pidx == ACKPPO_OFF_LOG_STD || pidx == ACKPPO_OFF_LOG_STD + 1) s -= ent_coef;
-    grad[pidx] = s;
-  }
-  if (blockIdx.x == 0) {
-    // loss rows: 32 block-strided groups x 8 slots in parallel (a serial loop over the rows was
-    // a chain of dependent L2 round trips: 28 us at 256 rows), then an LDS tree over the groups
-    static_assert(ACKPPO_NLOSS == 8, "loss row layout");
-    __shared__ float lred[256];
-    const int slot = threadIdx.x & 7, grp = threadIdx.x >> 3;
-    float s = 0.0f;
-    for (int b = grp; b < nblk; b += 32) s += lpart[(size_t)b * ACKPPO_NLOSS + slot];
-    lred[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o >= 8; o >>= 1) {
-      if (threadIdx.x < o) lred[threadIdx.x] += lred[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x < ACKPPO_NLOSS) loss[threadIdx.x] = (accumulate ? loss[threadIdx.x] : 0.0f) + lred[threadIdx.x];
   }
 }
 
@@ -1929,16 +1839,8 @@ int ackppo_grad_blocks(int batch) {
 namespace {
 int reduce_launch(float* grad_partial, const float* loss_partial, int nblk, float ent_coef, float* grad,
                   float* loss, int accumulate, void* stream) {
-  if (AK_PPO_REDUCE1) {
-    hipLaunchKernelGGL(ackppo_reduce1_kernel, dim3((P + R1_PB - 1) / R1_PB), dim3(R1_P * R1_G), 0, (hipStream_t)stream,
-                       grad_partial, nblk, loss_partial, ent_coef, grad, loss, accumulate);
-    return launched("ackppo_reduce");
-  }
-  const int rg = nblk < REDUCE_RG ? nblk : REDUCE_RG;
-  hipLaunchKernelGGL(ackppo_reduce_rows_kernel, dim3((P + 255) / 256, rg), dim3(256), 0, (hipStream_t)stream,
-                     grad_partial, nblk);
-  hipLaunchKernelGGL(ackppo_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, grad_partial, rg,
-                     loss_partial, nblk, ent_coef, grad, loss, accumulate);
+  hipLaunchKernelGGL(ackppo_reduce1_kernel, dim3((P + R1_P - 1) / R1_P), dim3(R1_P * R1_G), 0, (hipStream_t)stream,
+                     grad_partial, nblk, loss_partial, ent_coef, grad, loss, accumulate);
   return launched("ackppo_reduce");
 }
 }  // namespace
