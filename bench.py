@@ -217,32 +217,62 @@ def to_f64_state(st: torch.Tensor) -> np.ndarray:
 
 
 TOL_QPOS, TOL_QVEL = 1e-5, 1e-3  # tests/test_gpu_parity.py's stated f32 tolerances
+BOUNDARY_DZ = (1e-7, -1e-7, 1e-6, -1e-6)  # tests/test_gpu_parity.py's contact-activation boundary rule
+
+
+def boundary_excused(o, before_e, act_e, after_e, flags, seed) -> bool:
+    """The parity tests' excuse (tests/test_gpu_parity.py _boundary_excused): an env-step
+    over the tolerances counts as a contact-activation boundary case only if the oracle, with the body
+    shifted <= 1e-6 m in z, reproduces the GPU step within the same tolerances."""
+    for dz in BOUNDARY_DZ:
+        s = before_e[None].copy()
+        s[0, 2] += dz
+        o.step(s, act_e[None], flags=flags, seed=seed)
+        if (np.abs(after_e[:13] - s[0, :13]).max() <= TOL_QPOS and
+                np.abs(after_e[13:25] - s[0, 13:25]).max() <= TOL_QVEL):
+            return True
+    return False
 
 
 def parity_sample(o, device, contacts, flags, seed, n, steps, settle=0, drift=True):
     """Teacher-forced parity on a sample (same flags / seed as the timed run): every step starts the
-    oracle from the GPU's state; max errors and the env-steps over the stated tolerances (contact
-    activation boundaries, DESIGN.md §5, can exceed them; the parity tests excuse and cap those)."""
+    oracle from the GPU's state. An env-step over the stated tolerances is classified with the parity
+    tests' rule: excused (a contact-activation boundary, DESIGN.md §5: the oracle reproduces the GPU
+    step from the state shifted <= 1e-6 m in z) or unexcused; the max errors are over the env-steps
+    within tolerance and, separately, over all of them (raw)."""
     sim = BatchedAckermannSim(n, device, seed=seed, contacts=contacts)
     sim.reset()
     acts = sim.random_actions(settle + steps, seed=seed)
     if settle:
         sim.rollout(acts[:settle], want_info=False, per_step_outputs=False)
-    eq = ev = eo = 0.0
-    over = 0
+    eq = ev = eo = rq = rv = 0.0
+    excused = unexcused = 0
     for k in range(settle, settle + steps):
         s_before = to_f64_state(sim.state)
         sim.step(acts[k], want_info=False)
         torch.cuda.synchronize(device)
         s_after = to_f64_state(sim.state)
-        oobs, orew, _, _, _, _ = o.step(s_before, acts[k].cpu().numpy(), flags=flags, seed=seed)
-        dq = np.abs(s_after[:, 0:13] - s_before[:, 0:13]).max(1)
-        dv = np.abs(s_after[:, 13:25] - s_before[:, 13:25]).max(1)
-        over += int(((dq > TOL_QPOS) | (dv > TOL_QVEL)).sum())
-        eq, ev = max(eq, float(dq.max())), max(ev, float(dv.max()))
-        eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs).max()))
+        ref = s_before.copy()
+        a_np = acts[k].cpu().numpy()
+        oobs, orew, _, _, _, _ = o.step(ref, a_np, flags=flags, seed=seed)
+        dq = np.abs(s_after[:, 0:13] - ref[:, 0:13]).max(1)
+        dv = np.abs(s_after[:, 13:25] - ref[:, 13:25]).max(1)
+        ok = (dq <= TOL_QPOS) & (dv <= TOL_QVEL)
+        for e in np.nonzero(~ok)[0]:
+            if boundary_excused(o, s_before[e], a_np[e], s_after[e], flags, seed):
+                excused += 1
+            else:
+                unexcused += 1
+        rq, rv = max(rq, float(dq.max())), max(rv, float(dv.max()))
+        eq, ev = max(eq, float(dq[ok].max(initial=0.0))), max(ev, float(dv[ok].max(initial=0.0)))
+        eo = max(eo, float(np.abs(sim.obs_soa.cpu().numpy().T - oobs)[ok].max(initial=0.0)))
     out = {"max_abs_qpos_err": eq, "max_abs_qvel_err": ev, "max_abs_obs_err": eo,
-           "env_steps_over_tolerance": over, "tolerance": {"qpos": TOL_QPOS, "qvel": TOL_QVEL},
+           "env_steps_over_tolerance": excused + unexcused, "excused_boundary_env_steps": excused,
+           "unexcused_env_steps": unexcused, "raw_max_abs_qpos_err": rq, "raw_max_abs_qvel_err": rv,
+           "tolerance": {"qpos": TOL_QPOS, "qvel": TOL_QVEL},
+           "classification": "tests/test_gpu_parity.py rule: an over-tolerance env-step is excused only if the "
+                             "oracle reproduces the GPU step from the state shifted <= 1e-6 m in z (contact "
+                             "activation boundary); max_abs_* are over the env-steps within tolerance, raw_* over all",
            "sample": f"{n} envs x {steps} teacher-forced steps, contacts {'on' if contacts else 'off'}, "
                      + (f"after {settle} settle steps" if settle else "from reset") + " (f32 GPU vs f64 oracle)"}
     if drift:
@@ -389,7 +419,7 @@ def mfma_summary():
     out = {k: {"mfma_util": v.get("mfma_util"), "mfma_tflops": v.get("mfma_tflops"),
                "peak_tflops": v.get("f32_mfma_peak_tflops"), "duration_us": v.get("median_duration_ns", 0) / 1e3}
            for k, v in d.items() if isinstance(v, dict) and k.startswith("ackppo")}
-    out["source"] = f"profiles/mfma_latest.json ({d.get('_round', '?')}; rocprofv3 --pmc on tools/ppo_kbench.py)"
+    out["source"] = f"profiles/mfma_latest.json ({d.get('_round', '?')}; rocprofv3 --pmc on tools/ppo_train_workload.py: PPO.train() as the product runs it)"
     out["note"] = ("the physics step kernels use no MFMA (per-lane scalar f32 work); the PPO learner's GEMM-shaped "
                    "layers run v_mfma_f32_16x16x4_f32")
     return out

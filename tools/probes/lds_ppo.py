@@ -1,5 +1,6 @@
-"""LDS bank conflicts and waits of the PPO gradient launch (GPU box): one rocprofv3 --pmc pass over
-tools/ppo_kbench.py (ackppo_grad1 on an 8192-sample minibatch, 23 launches), per-kernel means.
+"""LDS bank conflicts and waits of the PPO update launches (GPU box): one rocprofv3 --pmc pass over
+tools/ppo_train_workload.py (PPO.train() as the product runs it: ackppo_grad1i_kernel per 8192-sample
+minibatch, 3 x 160 launches), per-kernel means.
 
     python3 tools/probes/lds_ppo.py
 
@@ -15,8 +16,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB = os.path.join(ROOT, "mujoco_playground_amd", "csrc", "build", "libackppo.so")
-KERNELS = ("ackppo_grad1_kernel", "ackppo_act_kernel", "ackppo_reduce_norm", "ackppo_adam_blocked_kernel")
+KERNELS = ("ackppo_grad1i_kernel", "ackppo_reduce_norm", "ackppo_adam_blocked_kernel")
 COUNTERS = ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS", "SQ_WAVES",
             "SQ_WAVE_CYCLES"]
 
@@ -24,8 +24,8 @@ COUNTERS = ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_LDS", "SQ_WAI
 def main():
     out = os.path.join(ROOT, "gpurun_out", "lds_ppo")
     os.makedirs(out, exist_ok=True)
-    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *COUNTERS, "--output-format", "csv", "-d", out, "-o",
-           "p", "--", sys.executable, os.path.join(ROOT, "tools", "ppo_kbench.py"), LIB]
+    cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--pmc", *COUNTERS, "--output-format", "csv", "-d", out, "-o",
+           "p", "--", sys.executable, os.path.join(ROOT, "tools", "ppo_train_workload.py")]
     subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL)
     per = {}
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
@@ -47,6 +47,7 @@ def main():
             m["lds_insts_per_wave"] = m["SQ_INSTS_LDS"] / m["SQ_WAVES"]
             m["wave_cycles_per_wave"] = m["SQ_WAVE_CYCLES"] / m["SQ_WAVES"]
         res[k] = m
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "lds_ppo_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 

@@ -1,8 +1,10 @@
 """MFMA utilisation of the PPO kernels (north_star: "MFMA util where used") -> gpurun_out/mfma_latest.json.
 
-Runs tools/ppo_kbench.py (ackppo_grad on an 8192-sample minibatch, ackppo_reduce, ackppo_adam and
-ackppo_act on 4096 envs, 23 launches each) under rocprofv3, one pass per counter group,
-kernel-trace only:
+Runs tools/ppo_train_workload.py -- PPO.train() as the product runs it (ackppo_train with the weight
+image: ackppo_grad1i_kernel per 8192-sample minibatch, then the reduction and Adam launches; the
+rollout's policy runs inside ackphys_ppo_rollout_quad_kernel) -- under rocprofv3, one pass per
+counter group, kernel-trace only (the round-5 figures were of ackppo_grad1_kernel,
+which tools/ppo_kbench.py launches and PPO.train does not):
   pass 1  SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F32, SQ_INSTS_VALU_MFMA_F32, GRBM_GUI_ACTIVE
   pass 2  the derived MfmaUtil (ROCm's formula: sum MFMA busy cycles / (max GRBM_GUI_ACTIVE x SIMDs))
   pass 3  --kernel-trace --stats (durations)
@@ -18,15 +20,15 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "mujoco_playground_amd", "csrc", "build", "libackppo.so")
-KERNELS = ("ackppo_grad1_kernel", "ackppo_act_kernel")
+KERNELS = ("ackppo_grad1i_kernel", "ackppo_reduce_norm128_kernel", "ackppo_adam_blocked_kernel",
+           "ackppo_perm_stats_kernel")
 SIMDS, XCDS, F32_MFMA_PEAK_TFLOPS = 1024, 8, 157.3
 
 
 def rocprof(args, out):
     os.makedirs(out, exist_ok=True)
-    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", *args, "--output-format", "csv", "-d", out, "-o", "p", "--",
-           sys.executable, os.path.join(ROOT, "tools", "ppo_kbench.py"), LIB]
+    cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", *args, "--output-format", "csv", "-d", out, "-o", "p", "--",
+           sys.executable, os.path.join(ROOT, "tools", "ppo_train_workload.py")]
     subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL)
 
 
@@ -83,7 +85,9 @@ def main():
                   "mfma_util": busy / (gui / XCDS * SIMDS) if gui else None,
                   "mfma_util_rocprof_derived_pct": (sum(d.get("MfmaUtil", 0.0) for d in dv) / len(dv)) if dv else None,
                   "mfma_tflops": mops * 512 / (ns * 1e-9) / 1e12, "f32_mfma_peak_tflops": F32_MFMA_PEAK_TFLOPS,
-                  "workload": "tools/ppo_kbench.py: grad = one 8192-sample minibatch (512 one-net workgroups of 32 samples), act = 4096 envs"}
+                  "workload": "tools/ppo_train_workload.py: 3 PPO.train() calls (ackppo_train, weight image), "
+                              "4096 envs x 32 steps, batch 8192 (256 two-tile one-net workgroups per minibatch), "
+                              "10 epochs = 160 minibatches per call"}
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "mfma_latest.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
