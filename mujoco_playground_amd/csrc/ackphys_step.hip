@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ackphys_model_gen.h"
 #include "ackphys_scene_gen.h"
 
