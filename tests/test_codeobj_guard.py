@@ -5,8 +5,13 @@ flat load of a private slot returned the neighbouring slot; a select table place
 back zeros), and the fixes were source idioms only. This test makes the invariant automatic: it
 extracts the gfx950 code object from each library the product loads (libackphys.so,
 libackppo.so: the `.hip_fatbin` section, unbundled with clang-offload-bundler), reads every
-kernel's AMDGPU metadata (llvm-readelf --notes) and fails if any kernel has a private segment, a
-dynamic stack, or a scratch instruction in its disassembly.
+kernel's AMDGPU metadata (llvm-readelf --notes) and fails if any kernel has a dynamic stack, or an
+instruction that can reach private memory in its disassembly: on gfx950 (architected flat scratch,
+no private-segment buffer) that is a `scratch_*` instruction or a `flat_*` one (a flat address can
+point into the private aperture -- the round-4 bug). A private segment the code never touches is
+reported, not failed: the backend reserves an emergency register-scavenging slot in kernels with
+heavy SGPR spilling to VGPR lanes (the flat per-step quad kernel in round 6: 68 bytes, no scratch or
+flat instruction), and the instruction check is the invariant that matters.
 
 Register spills that stay in registers are reported, not failed: with a zero private segment a
 `.vgpr_spill_count` is VGPRs parked in AGPRs (v_accvgpr_write/read) and an `.sgpr_spill_count` is
@@ -59,7 +64,7 @@ def kernel_metadata(co: str) -> dict:
 
 
 def scratch_instructions(co: str) -> dict:
-    """{kernel: number of scratch_* / private buffer instructions} from the disassembly."""
+    """{kernel: number of instructions that can reach private memory: scratch_* and flat_*}."""
     dis = subprocess.run([_tool("llvm-objdump"), "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
                          text=True).stdout
     out, cur = {}, None
@@ -69,7 +74,7 @@ def scratch_instructions(co: str) -> dict:
             cur = m.group(1)
             out.setdefault(cur, 0)
             continue
-        if cur and re.match(r"\s+scratch_", line):
+        if cur and re.match(r"\s+(scratch|flat)_", line):
             out[cur] += 1
     return out
 
@@ -103,9 +108,11 @@ def test_every_loaded_kernel_found(libs):
 def test_no_private_memory(libs, lib):
     md, scr = libs[lib]
     bad = {k: (v.get("private_segment_fixed_size"), v.get("uses_dynamic_stack"), scr.get(k, 0))
-           for k, v in md.items()
-           if v.get("private_segment_fixed_size", 0) or v.get("uses_dynamic_stack") or scr.get(k, 0)}
-    assert not bad, f"kernels with scratch (private segment B, dynamic stack, scratch instructions): {bad}"
+           for k, v in md.items() if v.get("uses_dynamic_stack") or scr.get(k, 0)}
+    assert not bad, f"kernels that can reach private memory (private segment B, dynamic stack, scratch/flat instructions): {bad}"
+    untouched = {k: v.get("private_segment_fixed_size") for k, v in md.items() if v.get("private_segment_fixed_size", 0)}
+    if untouched:
+        print(f"{lib}: private segments no instruction touches (scavenging slots): {untouched}")
 
 
 # register-resident spills of the hot kernels at this commit (VGPR -> AGPR, SGPR -> VGPR lane):
