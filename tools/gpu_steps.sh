@@ -35,9 +35,11 @@ for step in "$@"; do
       else run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread; fi ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench)
-      timeout -k 10 600 python -u bench.py ${val//,/ } > "gpurun_out/${TAG}_bench.json" 2> "gpurun_out/${TAG}_bench.err" \
-        || { echo "STEP_FAIL bench"; tail -30 "gpurun_out/${TAG}_bench.err"; exit 1; }
-      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('bench', round(d['value']/1e6,1), 'M', {k: (round(d[k]['value']/1e6,2) if d.get(k) else None) for k in ('secondary','obstacles','ppo')})" "gpurun_out/${TAG}_bench.json" ;;
+      # bench with flags writes TAG_bench_<flags>.json, so two bench steps of one call keep both lines
+      bn="${TAG}_bench"; [ -n "$val" ] && bn="${TAG}_bench_$(echo "$val" | tr -c 'a-zA-Z0-9\n' '_' | tr -s '_')"
+      timeout -k 10 600 python -u bench.py ${val//,/ } > "gpurun_out/${bn}.json" 2> "gpurun_out/${bn}.err" \
+        || { echo "STEP_FAIL bench"; tail -30 "gpurun_out/${bn}.err"; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('bench', sys.argv[1], round(d['value']/1e6,1), 'M', {k: (round(d[k]['value']/1e6,2) if d.get(k) else None) for k in ('secondary','obstacles','ppo')})" "gpurun_out/${bn}.json" ;;
     prof)
       (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o b -- python3 "$R/bench.py" --no-cpu > "$R/gpurun_out/${TAG}_prof.log" 2>&1) \
         || { echo "STEP_FAIL prof"; tail -20 "gpurun_out/${TAG}_prof.log"; exit 1; }
