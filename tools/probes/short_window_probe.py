@@ -2,7 +2,8 @@
 (`--steps 20 --warmup 5`), under different preludes: a fresh sim right after start-up, after the
 ~0.2 s clock warm-up on a throwaway sim, and back to back. Prints one JSON line per window.
 With `spin` the HIP runtime is asked to spin-wait on synchronisation (hipDeviceScheduleSpin)
-before anything touches the GPU.
+before anything touches the GPU. The last passes poll the end event (hipEventQuery) from the host
+before the synchronise ("query": true) against the plain synchronise.
 
     python tools/probes/short_window_probe.py [spin]
 """
@@ -39,24 +40,31 @@ def window(dev, tag, keep=None):
         sim.rollout(timed, want_info=False, per_step_outputs=False)
     t_launch = time.perf_counter()
     ev1.record()
+    if QUERY:  # poll the end event from the host before the synchronise
+        while not ev1.query():
+            pass
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     gc.enable()
-    print(json.dumps({"prelude": tag, "fast": FAST, "host_us": round((t1 - t0) * 1e6, 1), "launch_call_us": round((t_launch - t0) * 1e6, 1),
+    print(json.dumps({"prelude": tag, "fast": FAST, "query": QUERY, "host_us": round((t1 - t0) * 1e6, 1), "launch_call_us": round((t_launch - t0) * 1e6, 1),
                       "event_us": round(ev0.elapsed_time(ev1) * 1e3, 1)}), flush=True)
     if keep is not None:
         keep.append(sim)
 
 
 FAST = False
+QUERY = False
 
 
 def main():
-    global FAST
+    global FAST, QUERY
     if len(sys.argv) > 1 and sys.argv[1] == "spin":
         hip = ctypes.CDLL("libamdhip64.so")
         print(json.dumps({"hipSetDeviceFlags(spin)": hip.hipSetDeviceFlags(ctypes.c_uint(1))}), flush=True)
     for FAST in (False, True):
+        run()
+    FAST = True
+    for QUERY in (True, False, True):
         run()
 
 
