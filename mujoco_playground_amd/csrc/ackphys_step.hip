@@ -2221,7 +2221,7 @@ template <int NC>
 __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* xch, int* xflag, uint8_t* sh_bad,
                                               const uint8_t* sh_reset, int lane, int e, bool valid, int slot,
                                               int npair) {
-  STAMP_SCOPE
+  STAMP_SCOPE_A(A)
   const int n = A.n;
   Slots S{lds + lane};
   const uint32_t vo = 4u * (uint32_t)e;
@@ -2341,7 +2341,7 @@ __device__ __forceinline__ void step_dyn_wave(const Args& A, float* lds, float* 
 
 __device__ __forceinline__ void step_obs_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad,
                                               uint8_t* sh_reset, int lane, int e, bool valid, int slot, int npair) {
-  STAMP_SCOPE
+  STAMP_SCOPE_A(A)
   __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
@@ -2475,7 +2475,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) ackphys_step_serial_kernel(A
 template <int NC>
 __device__ __forceinline__ void step_prep_wave(const Args& A, float* xch, int* xflag, const uint8_t* sh_bad, int lane,
                                                int e, bool valid) {
-  STAMP_SCOPE
+  STAMP_SCOPE_A(A)
   __syncthreads();  // barrier 0 (see step_dyn_wave)
   const int n = A.n;
   const uint32_t vo = 4u * (uint32_t)e;
@@ -2629,6 +2629,9 @@ __device__ __forceinline__ void rollout_split(const Args& A) {
     B.sm_out = k + 1 < A.ksteps;
     B.nctrl = nctrl;
     B.next_action = k + 1 < A.ksteps ? A.action + (size_t)(k + 1) * 2 * A.n : nullptr;
+#ifdef AK_STAMPS  // the stamps kept are a mid-rollout step's (state into the LDS mirror, not HBM)
+    B.stamp_skip = A.ksteps > 1 && k != A.ksteps - 2;
+#endif
     step_split<NC, PW>(B);
   }
 }

@@ -1,7 +1,9 @@
 """Per-phase cycle breakdown of ackphys_step_kernel from the stamped diagnostic build.
 
     tools/build_diag.sh && python tools/stamps.py [quad|obst]
-    (STAMPS_ROLLOUT=K: the last step of K-step ackphys_rollout launches; STAMPS_JSON=path: merge the
+    (STAMPS_ROLLOUT=K: step K - 1 of K-step ackphys_rollout launches for the lane kernels, a mid-rollout
+    step whose state goes to the LDS mirror; the last step for the quad kernels, which store the state
+    every step; STAMPS_JSON=path: merge the
     per-kernel summaries into that file, e.g. profiles/critical_path_latest.json)
 Phases (stamp k -> k+1): 0 load/controller, 1 kinematics->dynamics entry, 2 M/bias/a0,
 3 contacts, 4 rows+warmstart, 5 Newton, 6 force+Euler solve, 7 (return) -> 8 obs prep,
@@ -15,7 +17,7 @@ import numpy as np
 import torch
 
 NSTAMP = 24  # AK_NSTAMP of the diagnostic build
-ROLL = int(os.environ.get("STAMPS_ROLLOUT", "1"))  # > 1: stamp the last step of an ackphys_rollout launch of ROLL steps
+ROLL = int(os.environ.get("STAMPS_ROLLOUT", "1"))  # > 1: stamp one step of an ackphys_rollout launch of ROLL steps
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
@@ -41,7 +43,9 @@ QUAD_PHASES = [(0, 1, "load+controller"), (1, 2, "kinematics"), (2, 3, "M/bias/a
 def main():
     quad = len(sys.argv) > 1 and sys.argv[1] in ("quad", "obst")
     obst = len(sys.argv) > 1 and sys.argv[1] == "obst"
-    phases = QUAD_PHASES if quad else PHASES
+    # lane rollout: the stamped step is a mid-rollout one (no HBM state store; its span ends past the barriers)
+    mid = ROLL > 1 and not quad
+    phases = QUAD_PHASES if quad else ([ph for ph in PHASES if ph[2] != "state store"] if mid else PHASES)
     L = C.CDLL(os.path.join(REPO, "diag_libs", os.environ.get("DIAG_LIB", "libackphys_stamps.so")))
     P = C.c_void_p
     L.ackphys_create.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(P)]
@@ -84,7 +88,7 @@ def main():
         res, spans = [], []
         for k in range(200, 210):
             stamps.zero_()
-            if ROLL > 1:  # the stamps left are those of the launch's last step
+            if ROLL > 1:  # the stamps left are those of step ROLL - 1 (lane) or of the last step (quad)
                 L.ackphys_rollout(ctx, ROLL, p(acts[k]), p(state), p(obs), p(rew), p(term), p(trunc), None, None, None,
                                   flags, 0, 0, stream)
             else:
@@ -94,7 +98,7 @@ def main():
             allv = stamps.cpu().numpy()
             s = allv[: NSTAMP * nb].reshape(NSTAMP, nb)
             res.append(np.stack([s[b] - s[a] for a, b, _ in phases]))
-            spans.append(s[10] - s[0] if not quad else np.sum(res[-1], axis=0))
+            spans.append(np.sum(res[-1], axis=0) if quad else (s[9] - s[0] if mid else s[10] - s[0]))
             its = allv[NSTAMP * nb:NSTAMP * nb + 64 * nb]
             nt = allv[NSTAMP * nb + 64 * nb:].reshape(5, nb)
             if k == 200:
@@ -140,7 +144,9 @@ def main():
                           "dyn_wave_cycles_per_step_max": float(np.max(np.concatenate(spans))),
                           "phases_median": {name: float(v) for (_, _, name), v in zip(phases, d)},
                           "measured": "diag build (s_memtime stamps, ~+11 % cycles), 4096 envs, steps 200-209 after "
-                                      "reset, " + (f"last step of {ROLL}-step rollout launches" if ROLL > 1
+                                      "reset, " + ((f"step {ROLL - 1} of {ROLL}-step rollout launches (mid-rollout: "
+                                                    "the state into the LDS mirror)" if mid else
+                                                    f"last step of {ROLL}-step rollout launches") if ROLL > 1
                                                    else "single-step launches")}
     if os.environ.get("STAMPS_JSON"):  # merged into the file's other entries (one file for every kernel)
         import json
