@@ -2976,7 +2976,7 @@ int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32
   const bool var = ctx->prm.action_repeat > 1 || ctx->prm.nohit_clear;
   hipLaunchKernelGGL(ctx->scene == 1 ? (var ? ackphys_ppo_rollout_obst8_var_kernel : ackphys_ppo_rollout_obst8_kernel)
                                      : (var ? ackphys_ppo_rollout_quad_var_kernel : ackphys_ppo_rollout_quad_kernel),
-                     dim3(blocks), dim3(128), 0, (hipStream_t)stream, a, P);
+                     dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, P);  // 16 envs, 4 waves (ppo_rollout)
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hipfail(e, "ackphys_ppo_rollout launch");
   return ACKPHYS_OK;
