@@ -48,7 +48,9 @@ __shared__ unsigned long long ak_stamp_lds[4][AK_NSTAMP];
   } while (0)
 struct StampScope {
   bool on;
-  __device__ explicit StampScope(bool on_ = true) : on(on_) {
+  // four-wave workgroups (the fused PPO rollout: dynamics waves 0-1, observation waves 2-3) flush
+  // waves 0 and 2 only: the stamp rows are per workgroup
+  __device__ explicit StampScope(bool on_ = true) : on(on_ && !(blockDim.x == 256 && ((threadIdx.x >> 6) & 1))) {
     if ((threadIdx.x & 63) == 0)
       for (int k = 0; k < AK_NSTAMP; k++) ak_stamp_lds[threadIdx.x >> 6][k] = 0;
   }

@@ -1,7 +1,8 @@
 """Where a fused PPO rollout step's time goes (stamped diagnostic build, tools/build_diag.sh): per
 workgroup, the cycles of the dynamics wave (state loaded -> barrier 1) against the observation
 wave's observation, TimeLimit bootstrap and policy (all before barrier 1), for step T - 2 of an
-n_steps rollout (the last step runs the critic alone). 4096 envs, 8 per workgroup.
+n_steps rollout (the last step runs the critic alone). 4096 envs, 16 per workgroup: the stamps are
+those of dynamics wave 0 and observation wave 2 (the actor's; the diagnostic build flushes no others).
 
     python tools/probes/ppo_rollout_stamps.py [flat|obstacles]
 """
@@ -28,7 +29,7 @@ def main(scene):
     n = 4096
     venv = AckermannVecEnv(n, device=dev, seed=0, contacts=True, scene=scene)
     model = PPO("MlpPolicy", venv, n_steps=32, batch_size=8192, n_epochs=10, seed=0)
-    nb = (n + 7) // 8
+    nb = (n + 15) // 16
     stamps = torch.zeros(NSTAMP * nb + nb * 64 + 5 * nb, dtype=torch.int64, device=dev)
     assert L.ackphys_diag_set_stamps(C.c_void_p(stamps.data_ptr())) == 0
     for _ in range(3):  # past the first episodes' start-up
