@@ -10,7 +10,8 @@ own state, observation, episode statistics and last-step buffers are compared ex
 consecutive rollouts (the second starts from the first's last_dones and step counter). Short
 episodes (truncation -> TimeLimit bootstrap and auto-reset inside the launch), a goal threshold that
 terminates some episodes at once (termination: no bootstrap), ragged N (not a multiple of the
-8-env workgroup), both scenes, and envs whose state trips mj_checkAcc (the redo barrier).
+16-env workgroup, including a last workgroup whose second observation wave and dynamics wave hold no
+env), both scenes, and envs whose state trips mj_checkAcc (the redo barrier).
 """
 import pytest
 import torch
@@ -48,9 +49,9 @@ def _compare(a, b, tag):
     assert torch.equal(a.sim.terminal_obs_soa[:, done], b.sim.terminal_obs_soa[:, done]), f"{tag}: terminal obs"
 
 
-@pytest.mark.parametrize("scene", ["flat", "obstacles"])
-def test_fused_rollout_equals_per_step(scene):
-    n, T = 301, 23
+@pytest.mark.parametrize("scene,n", [("flat", 301), ("obstacles", 301), ("flat", 35)])
+def test_fused_rollout_equals_per_step(scene, n):
+    T = 23
     a, b = _pair(n, scene, T, eplen=9, thr=2.4)
     assert a.fused_rollout and not b.fused_rollout
     for it in range(2):
