@@ -2692,6 +2692,7 @@ struct ackphys_ctx {
   ak::EnvParams prm;
   int variant;  // ACKPHYS_VARIANT_LANE (1 lane/env) or ACKPHYS_VARIANT_QUAD (4 lanes/env)
   int scene;    // 0: ackermann_robot_v2 (floor only); 1: obstacle scene (floor + boxes)
+  float* pimg = nullptr;  // ackphys_ppo_rollout: the policy's weight image (allocated at the first call)
 };
 
 static thread_local char g_err[512];
@@ -2777,6 +2778,10 @@ int ackphys_create(const void* model_blob, size_t nbytes, int n_env, int device,
 }
 
 int ackphys_destroy(ackphys_t* ctx) {
+  if (ctx && ctx->pimg) {
+    DeviceGuard dg(ctx->device);
+    (void)hipFree(ctx->pimg);
+  }
   delete ctx;
   return ACKPHYS_OK;
 }
@@ -2972,8 +2977,18 @@ int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32
   if (dg.err != hipSuccess) return hipfail(dg.err, "hipSetDevice");
   ak::Args a{nullptr, state, obs, reward, term, trunc, terminal_obs, nullptr, episode, ctx->prm, ctx->n_env, flags,
              seed, ctx->env_offset, ak::PPO_PE};
+  if (!ctx->pimg) {
+    const hipError_t me = hipMalloc(&ctx->pimg, sizeof(float) * ak::PIMG_N);
+    if (me != hipSuccess) {
+      ctx->pimg = nullptr;
+      return hipfail(me, "ackphys_ppo_rollout: weight image");
+    }
+  }
+  // the weights as the policy's MFMA operands, from this call's parameters (they change every update)
+  hipLaunchKernelGGL(ak::ackphys_policy_image_kernel, dim3((ak::PIMG_N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     params, ctx->pimg);
   ak::PpoArgs P{params, policy_seed, step0, deterministic, gamma, n_steps, obs_rows, actions, log_prob, value,
-                rollout_reward, episode_starts, last_dones, last_values};
+                rollout_reward, episode_starts, last_dones, last_values, ctx->pimg};
   const int blocks = (ctx->n_env + ak::PPO_PE - 1) / ak::PPO_PE;
   const bool var = ctx->prm.action_repeat > 1 || ctx->prm.nohit_clear;
   hipLaunchKernelGGL(ctx->scene == 1 ? (var ? ackphys_ppo_rollout_obst8_var_kernel : ackphys_ppo_rollout_obst8_kernel)
