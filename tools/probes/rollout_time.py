@@ -3,7 +3,7 @@ own child process (GPU box): ms per collect_rollouts() (4096 envs x 32 steps) an
 step (4096 envs, 200 steps in one launch), with checksums of the rollout buffers and the sim state
 (builds that should agree bit for bit can be compared).
 
-    python3 tools/probes/rollout_time.py LIBACKPHYS.so [...] [--reps 5]
+    python3 tools/probes/rollout_time.py LIBACKPHYS.so [...] [--reps 5] [--scene obstacles]
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 
 
-def child(lib, reps):
+def child(lib, reps, scene):
     sys.path.insert(0, REPO)
     from mujoco_playground_amd import _lib
     _lib.LIB_PATH = os.path.abspath(lib)
@@ -26,7 +26,7 @@ def child(lib, reps):
     from mujoco_playground_amd.rl.ppo import PPO
     from mujoco_playground_amd.sim import BatchedAckermannSim
     dev = torch.device("cuda:0")
-    venv = AckermannVecEnv(4096, device=dev, seed=0, contacts=True)
+    venv = AckermannVecEnv(4096, device=dev, seed=0, contacts=True, scene=scene)
     model = PPO("MlpPolicy", venv, n_steps=32, batch_size=8192, n_epochs=10, seed=0)
     for _ in range(2):
         model.collect_rollouts()
@@ -40,7 +40,7 @@ def child(lib, reps):
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     ck = float(model.buf_obs.double().abs().sum() + model.buf_act.double().abs().sum() + model.buf_rew.double().abs().sum())
-    sim = BatchedAckermannSim(4096, dev, seed=0, contacts=True)
+    sim = BatchedAckermannSim(4096, dev, seed=0, contacts=True, scene=scene)
     sim.reset()
     acts = sim.random_actions(400, seed=0)
     sim.rollout(acts[:200], want_info=False, per_step_outputs=False)
@@ -60,12 +60,13 @@ def main():
     ap.add_argument("libs", nargs="*")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--scene", default="flat")
     a = ap.parse_args()
     if a.child:
-        child(a.child, a.reps)
+        child(a.child, a.reps, a.scene)
         return
     for lib in a.libs:
-        r = subprocess.run([sys.executable, __file__, "--child", lib, "--reps", str(a.reps)], timeout=300)
+        r = subprocess.run([sys.executable, __file__, "--child", lib, "--reps", str(a.reps), "--scene", a.scene], timeout=300)
         if r.returncode:
             print(f"{lib}: exit {r.returncode}", flush=True)
             sys.exit(r.returncode)
