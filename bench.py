@@ -69,8 +69,8 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     if per_step or graph:
         for k in range(warmup):
             sim.step(actions[k], want_info=False)
-    elif warmup:
-        sim.rollout(actions[:warmup], want_info=False, per_step_outputs=False)
+    elif warmup:  # through a launcher like the timed one (the same C call, warmed before the window)
+        sim.rollout_launcher(actions[:warmup].contiguous(), want_terminal=True)()
     timed_actions = actions[warmup:]  # [K, N, 2], contiguous, resident before the timed region
     step_actions = timed_actions.unbind(0)  # per-step views, made before the timed region
     g = None
@@ -86,6 +86,7 @@ def run_gpu(n_env, steps, warmup, contacts, rank, world, device, seed=0, variant
     launch = None if (per_step or g is not None) else sim.rollout_launcher(
         timed_actions, outputs=sim.rollout_buffers(steps) if buffers else None)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev1.record(stream)  # the end event's HIP event is created here, not by its record inside the window
     torch.cuda.synchronize(device)
     shard.barrier(world, device)
     torch.cuda.synchronize(device)
