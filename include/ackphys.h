@@ -141,7 +141,10 @@ int ackphys_reset(ackphys_t* ctx, const uint8_t* mask, uint64_t seed, float* sta
  * (unclipped samples), log_prob / value / rollout_reward (with the TimeLimit bootstrap) /
  * episode_starts [T][N] (row 0 is the caller's: the previous rollout's last_dones), last_dones [N],
  * last_values [N]. Needs flags ACKPHYS_CONTACTS | ACKPHYS_AUTORESET (no ACKPHYS_POSTSTEP_OBS) and the
- * quad mapping (variant AUTO or QUAD). Replaces the reference's DummyVecEnv.step loop under SB3. */
+ * quad mapping (variant AUTO or QUAD). Replaces the reference's DummyVecEnv.step loop under SB3.
+ * The first call on a context allocates a 72 KB device buffer it keeps (the policy's weights in the
+ * kernel's operand order, rebuilt from params on the stream at every call; freed by
+ * ackphys_destroy), so calls on one context must not run concurrently on different streams. */
 int ackphys_ppo_rollout(ackphys_t* ctx, const float* params, int n_steps, uint32_t step0, uint64_t policy_seed,
                         int deterministic, float gamma, float* state, float* obs, float* reward, uint8_t* term,
                         uint8_t* trunc, float* terminal_obs, float* episode, float* obs_rows, float* actions,
